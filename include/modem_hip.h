@@ -1,0 +1,211 @@
+/*
+ * include/modem_hip.h — C ABI of the MI355X (gfx950) modem sample-path backend.
+ *
+ * This is the drop-in boundary for the hot path of ramtej/rust-modem (`src/modem`):
+ *   bits -> symbol index -> (I,Q) LUT -> zero-stuff + RRC pulse-shaping FIR -> carrier mix
+ *   -> [HBM sample buffer] -> conjugate mix -> matched filter at the decimated instants
+ *   -> hard decision.
+ * Every entry point is plain C: pointers, sizes, enums; no HIP or torch types (streams are
+ * passed as an opaque `void*` hipStream_t; NULL = the device's default stream), so a Rust
+ * `extern "C"` block, cgo or ctypes can bind it directly.
+ *
+ * Which reference interface each entry replaces (paths relative to the reference crate):
+ *   modem_freq_sample_freq   freq.rs:19-26           Freq::new(hz, sr).sample_freq()
+ *   modem_rates_sps          rates.rs:12-18          Rates::new(br, sr).samples_per_symbol
+ *   modem_carrier_phase      carrier.rs:17-26,       Carrier::inner(s) = mod_trig(w * s as f32)
+ *                            util.rs:3-6
+ *   modem_phasor_lut         digital/phasor.rs:1-12, the memoryless DigitalPhasor plugins
+ *                            bpsk.rs, qpsk.rs, qam.rs, bask.rs, mpsk.rs, apsk.rs, oqpsk.rs
+ *   modem_tx_*               modulator.rs:64-101     DigitalModulator::new(&mut Carrier,
+ *                            (+ fir.rs:3-35 for the   Box<DigitalPhasor>, Box<Source>) +
+ *                            pulse shaping)           Iterator<Item=IQSample>; IQSample::
+ *                                                     modulate (modulator.rs:45-48)
+ *   modem_rx_*               demodulator.rs:7-56     Demodulator::new(Carrier, S, Fn()->
+ *                                                     FIRFilter) + Iterator<Item=(f32,f32)>
+ *   modem_fir_*              fir.rs:3-35             FIRFilter::new(&[f32]) + add(f32)->f32
+ *
+ * Conventions
+ *   - Every function returns modem_status (0 = OK, negative = error) and never aborts.
+ *     Where the reference panics (assert!, unwrap, out-of-range), this ABI returns
+ *     MODEM_ERR_INVALID_ARG instead.
+ *   - Taps and LUTs are copied at create time; the caller may free them afterwards.
+ *   - I/O buffers are caller-owned. `*_process` accepts device pointers (asynchronous on
+ *     `stream`) or host pointers (staged through the handle's device buffers; the call then
+ *     synchronises `stream` before returning so the host buffers are valid).
+ *   - Streaming: consecutive `*_process` calls equal one long call (the handle carries the
+ *     carrier sample counter, the FIR history, leftover bits and the decimation phase);
+ *     `*_flush` drains the filter with zeros.
+ *   - One handle = one device; a handle is not thread-safe (it mirrors `&mut self`);
+ *     distinct handles may be driven from different host threads.
+ */
+#ifndef MODEM_HIP_H
+#define MODEM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MODEM_HIP_ABI_VERSION 1
+
+typedef enum {
+    MODEM_OK = 0,
+    MODEM_ERR_INVALID_ARG = -1,   /* the reference would panic (assert!/unwrap/index) */
+    MODEM_ERR_UNSUPPORTED = -2,   /* outside what this backend implements */
+    MODEM_ERR_HIP = -3,           /* a HIP runtime call failed */
+    MODEM_ERR_NO_DEVICE = -4,     /* no gfx950 device / bad device ordinal */
+    MODEM_ERR_CAPACITY = -5,      /* output buffer too small for the call */
+    MODEM_ERR_ALLOC = -6          /* host or device allocation failed */
+} modem_status;
+
+typedef enum { MODEM_DTYPE_F32 = 0, MODEM_DTYPE_F16 = 1 } modem_dtype;
+
+/* TX output: complex (i,q)*e^{j phase} (IQSample::modulate, modulator.rs:45-48); the
+ * un-mixed baseband (what `modulate --iq` writes, modulate.rs:110-113); or only the real
+ * part (what `modulate` writes by default, modulate.rs:128-133). */
+typedef enum {
+    MODEM_OUT_IQ_MIXED = 0,
+    MODEM_OUT_IQ_BASEBAND = 1,
+    MODEM_OUT_REAL = 2
+} modem_out_mode;
+
+/* RX mix: complex conjugate x*e^{-j phase} (loopback contract), or the reference's
+ * real-input mix x.re*(cos, -sin) with the 2x gain (demodulator.rs:46,52-55). */
+typedef enum { MODEM_MIX_COMPLEX = 0, MODEM_MIX_REFERENCE_REAL = 1 } modem_mix;
+
+typedef enum {
+    MODEM_SLICER_NONE = 0,        /* no decisions */
+    MODEM_SLICER_NEAREST = 1,     /* argmin |r - lut[s]|^2, lowest index on ties */
+    MODEM_SLICER_QAM_AXIS = 2     /* per-axis round+clamp, for QAM at phase 0 */
+} modem_slicer_kind;
+
+/* ---- memoryless DigitalPhasor plugins (host-side LUT builders) -------------------------- */
+typedef enum {
+    MODEM_PHASOR_BPSK = 1,   /* BPSK::new(phase, amplitude)            bpsk.rs:10-15 */
+    MODEM_PHASOR_QPSK = 2,   /* QPSK::new(phase, amplitude)            qpsk.rs:11-17 */
+    MODEM_PHASOR_QAM = 3,    /* QAM::new(bits_per_symbol, phase, amp)  qam.rs:15-30 */
+    MODEM_PHASOR_BASK = 4,   /* BASK::new(amplitude)                   bask.rs:8-12 */
+    MODEM_PHASOR_MPSK = 5,   /* MPSK::new(bps, phase_offset, amp)      mpsk.rs:14-21 */
+    MODEM_PHASOR_APSK = 6,   /* APSK::new(amplitude, bps, rings)       apsk.rs:25-33 */
+    MODEM_PHASOR_OQPSK = 7   /* OQPSK::new(amplitude) (symbol map only) oqpsk.rs:9-13 */
+} modem_phasor_kind;
+
+typedef struct { uint8_t start, end; float radius, phase; } modem_ring; /* apsk.rs:60-82 */
+
+typedef struct {
+    int32_t kind;                /* modem_phasor_kind */
+    uint32_t bits_per_symbol;    /* QAM/MPSK/APSK; implied for the others */
+    float phase;                 /* BPSK/QPSK/QAM phase, MPSK phase_offset */
+    float amplitude;
+    uint32_t nrings;             /* APSK */
+    const modem_ring* rings;     /* APSK */
+} modem_phasor_desc;
+
+/* Slicer description; fill it with modem_phasor_slicer() or by hand. */
+typedef struct {
+    int32_t kind;                /* modem_slicer_kind */
+    uint32_t bits_per_symbol;
+    const float* lut;            /* NEAREST: 2 * 2^bps floats (i,q), host memory */
+    uint32_t bits_per_carrier;   /* QAM_AXIS */
+    float inv_scale;             /* QAM_AXIS: 1 / QAM amplitude scale (qam.rs:28) */
+    float max_symbol;            /* QAM_AXIS: 2^bits_per_carrier - 1 */
+} modem_slicer_desc;
+
+const char* modem_status_str(modem_status s);
+int32_t modem_abi_version(void);
+
+/* Freq::new(hz, sr).sample_freq() — freq.rs:19-26 (f32, bit-exact). */
+float modem_freq_sample_freq(uint64_t hz, uint64_t sr);
+/* Rates::new(br, sr).samples_per_symbol — rates.rs:12-18. br == 0 -> INVALID_ARG. */
+modem_status modem_rates_sps(uint64_t br, uint64_t sr, uint64_t* sps);
+/* Carrier phase of absolute sample n, bit-exact to carrier.rs:17-19 + util.rs:3-6. */
+float modem_carrier_phase(float sample_freq, uint64_t n);
+/* The same phase for n consecutive samples s0.. computed by the device code path the
+ * kernels use (out: n floats, device pointer; asynchronous on stream). */
+modem_status modem_carrier_phases(float sample_freq, uint64_t s0, size_t n, float* out,
+                                  int device, void* stream);
+/* Bits per symbol of a phasor (DigitalPhasor::bits_per_symbol, phasor.rs:2). */
+modem_status modem_phasor_bits(const modem_phasor_desc* d, uint32_t* bps);
+/* (I,Q) table of a memoryless phasor: lut[2s], lut[2s+1] = i(_, b), q(_, b) where b are
+ * the bits of s MSB-first (bytes_to_bits, digital/util.rs:5-11). 2*2^bps floats. */
+modem_status modem_phasor_lut(const modem_phasor_desc* d, float* lut);
+/* Pick the cheapest exact slicer for a phasor: QAM_AXIS for QAM at phase 0, else NEAREST
+ * (lut must then stay valid until the RX handle is created). */
+modem_status modem_phasor_slicer(const modem_phasor_desc* d, const float* lut,
+                                 modem_slicer_desc* out);
+/* Root-raised-cosine taps (GLUE, absent from the reference): centred at (L-1)/2,
+ * roll-off beta, unit energy. */
+modem_status modem_rrc_taps(uint32_t ntaps, uint32_t sps, double beta, float* out);
+
+/* ---- TX: DigitalModulator + pulse shaping ------------------------------------------------ */
+typedef struct modem_tx modem_tx;
+typedef struct {
+    uint32_t bits_per_symbol;    /* 1..8 */
+    const float* lut;            /* 2 * 2^bps floats from modem_phasor_lut (host memory) */
+    uint32_t samples_per_symbol; /* Rates::samples_per_symbol, >= 1 */
+    const float* taps;           /* pulse-shaping FIR (host memory) */
+    uint32_t ntaps;              /* 0 = the reference's sample-and-hold (no FIR) */
+    float sample_freq;           /* Freq::sample_freq() of the carrier */
+    uint64_t s0;                 /* Carrier.sample at the first output sample */
+    int32_t dtype;               /* modem_dtype of the output samples */
+    int32_t out_mode;            /* modem_out_mode */
+} modem_tx_desc;
+
+modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out);
+/* Consume `nbits` bits (one byte per bit, values 0/1 — data.rs:36) and write
+ * floor((carry + nbits) / bps) * sps samples (2 values per sample for IQ modes, 1 for
+ * OUT_REAL, each f32 or f16). Leftover bits (< bps) carry into the next call.
+ * `cap` is in samples. */
+modem_status modem_tx_process(modem_tx* h, const uint8_t* bits, size_t nbits, void* out,
+                              size_t cap, size_t* produced, void* stream);
+/* Append ceil((ntaps-1)/sps) all-zero symbols so the FIR tail drains. */
+modem_status modem_tx_flush(modem_tx* h, void* out, size_t cap, size_t* produced, void* stream);
+/* Samples that the next call will start at (Carrier.sample, carrier.rs:6). */
+uint64_t modem_tx_sample(const modem_tx* h);
+modem_status modem_tx_destroy(modem_tx* h);
+
+/* ---- RX: Demodulator + matched filter + decimation + slicer ----------------------------- */
+typedef struct modem_rx modem_rx;
+typedef struct {
+    float sample_freq;           /* carrier (demodulator.rs:20) */
+    uint64_t s0;                 /* Carrier.sample of the first input sample */
+    const float* taps;           /* matched filter / lowpass (host memory) */
+    uint32_t ntaps;              /* >= 1 */
+    uint32_t decim;              /* keep every decim-th filter output; 1 = full rate */
+    uint32_t decim_offset;       /* keep outputs n = k*decim + decim_offset (stream index) */
+    int32_t mix;                 /* modem_mix */
+    int32_t in_dtype;            /* modem_dtype of the input I/Q samples */
+    int32_t out_dtype;           /* modem_dtype of the decimated I/Q output */
+    modem_slicer_desc slicer;    /* decisions (kind NONE for none) */
+} modem_rx_desc;
+
+modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out);
+/* Consume n complex input samples (interleaved i,q); write the decimated filter outputs
+ * (interleaved i,q; may be NULL) and u8 decisions (may be NULL) for every kept instant in
+ * this chunk. `cap` is in symbols. */
+modem_status modem_rx_process(modem_rx* h, const void* in, size_t n, void* out_iq,
+                              uint8_t* out_sym, size_t cap, size_t* produced, void* stream);
+/* Feed ntaps-1 zero samples (drains the matched filter). */
+modem_status modem_rx_flush(modem_rx* h, void* out_iq, uint8_t* out_sym, size_t cap,
+                            size_t* produced, void* stream);
+uint64_t modem_rx_sample(const modem_rx* h);
+modem_status modem_rx_destroy(modem_rx* h);
+
+/* ---- FIRFilter: real-valued causal FIR over a stream (fir.rs:3-35) ---------------------- */
+typedef struct modem_fir modem_fir;
+modem_status modem_fir_create(const float* taps, uint32_t ntaps, int device, modem_fir** out);
+/* out[i] = FIRFilter::add(in[i]) for consecutive samples (f32, same count in and out). */
+modem_status modem_fir_process(modem_fir* h, const float* in, float* out, size_t n, void* stream);
+modem_status modem_fir_destroy(modem_fir* h);
+
+/* ---- synthetic input (GLUE): splitmix64 bit stream, one byte per bit ------------------- */
+/* bit i = (word[i/64] >> (i%64)) & 1, word j = splitmix64 output j+1 from `seed`.
+ * `out` must be a device pointer. */
+modem_status modem_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, int device, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

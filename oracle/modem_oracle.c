@@ -1,0 +1,582 @@
+/*
+ * oracle/modem_oracle.c — TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * CPU restatement of ramtej/rust-modem `src/modem` (see modem_oracle.h for scope and
+ * pinning). Every function cites the reference file:line it restates; operation order
+ * follows the Rust source expression by expression (left-associative, no fused
+ * multiply-add: build with -ffp-contract=off, never -ffast-math).
+ * Nothing in the product (rust-modem_amd/) links or calls this file.
+ */
+#include "modem_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* std::f32::consts::PI (0x40490fdb) */
+#define OR_PI 3.14159265358979323846f
+
+/* ---- util.rs:3-6 ---------------------------------------------------------------------- */
+float or_mod_trig(float x) {
+    const float TWO_PI = OR_PI * 2.0f;                   /* util.rs:4 */
+    return x - TWO_PI * floorf(x / TWO_PI);              /* util.rs:5 */
+}
+
+/* ---- digital/util.rs:1-15 ------------------------------------------------------------- */
+float or_bit_to_sign(uint8_t b) {                         /* digital/util.rs:1-3 */
+    return (float)(int8_t)(2 * (int8_t)b - 1);
+}
+
+uint8_t or_bytes_to_bits(const uint8_t* bytes, size_t n) { /* digital/util.rs:5-11 */
+    if (n == 0) return 0;                                 /* fold over an empty slice */
+    size_t len = n - 1;
+    uint8_t s = 0;
+    for (size_t i = 0; i < n; i++) s = (uint8_t)(s | (uint8_t)((bytes[i] & 1) << (len - i)));
+    return s;
+}
+
+size_t or_max_symbol(size_t bps) { return ((size_t)1 << bps) - 1; } /* digital/util.rs:13-15 */
+
+/* ---- freq.rs / rates.rs / carrier.rs --------------------------------------------------- */
+float or_freq_ang_freq(size_t hz) { return 2.0f * OR_PI * (float)hz; }     /* freq.rs:19-21 */
+float or_freq_sample_freq(size_t hz, size_t sr) {                            /* freq.rs:24-26 */
+    return or_freq_ang_freq(hz) / (float)sr;
+}
+size_t or_rates_samples_per_symbol(size_t br, size_t sr) { return sr / br; } /* rates.rs:16 */
+
+void or_carrier_init(or_carrier* c, float sf, uint64_t sample) {            /* carrier.rs:10-15 */
+    c->sample_freq = sf; c->sample = sample;
+}
+float or_carrier_inner(const or_carrier* c, uint64_t s) {                   /* carrier.rs:17-19 */
+    return or_mod_trig(c->sample_freq * (float)s);        /* `s as f32`: round-to-nearest-even */
+}
+float or_carrier_next(or_carrier* c) {                                       /* carrier.rs:21-26 */
+    uint64_t sample = c->sample;
+    c->sample += 1;
+    return or_carrier_inner(c, sample);
+}
+void or_carrier_phases(float sf, uint64_t s0, size_t n, float* out) {
+    or_carrier c; or_carrier_init(&c, sf, s0);
+    for (size_t i = 0; i < n; i++) out[i] = or_carrier_next(&c);
+}
+
+/* ---- data.rs ---------------------------------------------------------------------------- */
+void or_symbol_clock_init(or_symbol_clock* c, size_t sps) {                 /* data.rs:20-25 */
+    c->samples_per_symbol = sps; c->counter = sps - 1;
+}
+int or_symbol_clock_next(or_symbol_clock* c) {                              /* data.rs:27-32 */
+    c->counter += 1;
+    c->counter %= c->samples_per_symbol;
+    return c->counter == 0;
+}
+
+void or_bits_init(or_bits_source* s, const uint8_t* bits, size_t nbits, size_t sps,
+                  size_t bps) {                                              /* data.rs:43-52 */
+    s->bits = bits; s->nbits = nbits; or_symbol_clock_init(&s->clock, sps);
+    s->bits_per_symbol = bps; s->idx = 0;
+}
+static const uint8_t* or_bits_slice(const or_bits_source* s) {              /* data.rs:54-63 */
+    size_t start = (s->idx - 1) * s->bits_per_symbol;
+    size_t end = start + s->bits_per_symbol;
+    return end <= s->nbits ? s->bits + start : NULL;
+}
+int or_bits_next(or_bits_source* s, const uint8_t** slice) {                 /* data.rs:66-78 */
+    if (or_symbol_clock_next(&s->clock)) {
+        s->idx += 1;
+        const uint8_t* b = or_bits_slice(s);
+        if (!b) return OR_FINISHED;
+        *slice = b; return OR_CHANGED;
+    }
+    *slice = or_bits_slice(s);                            /* `.unwrap()` at :76 */
+    return OR_UNCHANGED;
+}
+
+/* Rust `(b as char).is_whitespace()` for a byte (Unicode White_Space in U+0000..U+00FF). */
+static int or_is_whitespace(unsigned char c) {
+    return c == ' ' || (c >= 0x09 && c <= 0x0d) || c == 0x85 || c == 0xa0;
+}
+void or_ascii_init(or_ascii_bits* a, const char* text, size_t len, size_t sps, size_t bps) {
+    a->text = text; a->len = len; a->pos = 0;                                /* data.rs:132-140 */
+    or_symbol_clock_init(&a->clock, sps);
+    memset(a->bits, 0, sizeof a->bits); a->nbits = bps; a->panicked = 0;
+}
+static int or_ascii_next_bit(or_ascii_bits* a, uint8_t* bit) {              /* data.rs:142-159 */
+    for (;;) {
+        if (a->pos >= a->len) return 0;                   /* read() != Ok(1) */
+        unsigned char c = (unsigned char)a->text[a->pos++];
+        if (or_is_whitespace(c)) continue;
+        if (c != '0' && c != '1') { a->panicked = 1; return 0; }  /* assert! at :155 */
+        *bit = (uint8_t)(c - '0');
+        return 1;
+    }
+}
+int or_ascii_read_bits(or_ascii_bits* a) {                                   /* data.rs:161-171 */
+    for (size_t i = 0; i < a->nbits; i++) {
+        uint8_t b;
+        if (!or_ascii_next_bit(a, &b)) return 0;
+        a->bits[i] = b;
+    }
+    return 1;
+}
+int or_ascii_next(or_ascii_bits* a, const uint8_t** slice) {                 /* data.rs:174-185 */
+    if (or_symbol_clock_next(&a->clock)) {
+        if (or_ascii_read_bits(a)) { *slice = a->bits; return OR_CHANGED; }
+        return OR_FINISHED;
+    }
+    *slice = a->bits;
+    return OR_UNCHANGED;
+}
+
+int or_source_next(or_source* s, const uint8_t** slice) {                    /* data.rs:10-12 */
+    return s->is_ascii ? or_ascii_next(&s->ascii, slice) : or_bits_next(&s->bits, slice);
+}
+
+int or_even_odd_init(or_even_odd* e, const or_source* inner, size_t sps, size_t bps) {
+    if (bps != 2) return -1;                              /* data.rs:91 */
+    if (sps % bps != 0) return -1;                        /* data.rs:92 */
+    e->data = *inner;                                     /* data.rs:94-98 */
+    or_symbol_clock_init(&e->clock, sps / bps);
+    e->cur[0] = 0; e->cur[1] = 0;
+    return 0;
+}
+int or_even_odd_next(or_even_odd* e, const uint8_t** slice) {                /* data.rs:102-122 */
+    const uint8_t* b = NULL;
+    int u = or_source_next(&e->data, &b);
+    if (u == OR_FINISHED) return OR_FINISHED;             /* :105 */
+    if (u == OR_CHANGED) {                                /* :106-111 */
+        or_symbol_clock_next(&e->clock);
+        e->cur[0] = b[0];
+        *slice = e->cur; return OR_CHANGED;
+    }
+    if (or_symbol_clock_next(&e->clock)) {                /* :116-121 half-symbol update */
+        e->cur[1] = b[1];
+        *slice = e->cur; return OR_CHANGED;
+    }
+    *slice = e->cur;
+    return OR_UNCHANGED;
+}
+
+/* ---- digital/<x>.rs ------------------------------------------------------------------------ */
+static void or_phasor_zero(or_phasor* p, int kind) { memset(p, 0, sizeof *p); p->kind = kind; }
+
+int or_bpsk_new(or_phasor* p, float phase, float amplitude) {               /* bpsk.rs:10-15 */
+    or_phasor_zero(p, OR_BPSK); p->phase = phase; p->amplitude = amplitude;
+    p->bits_per_symbol = 1; return 0;
+}
+int or_qpsk_new(or_phasor* p, float phase, float amplitude) {               /* qpsk.rs:11-17 */
+    or_phasor_zero(p, OR_QPSK);
+    p->phase_cos = cosf(phase); p->phase_sin = sinf(phase);
+    p->amplitude = amplitude * sqrtf(0.5f);               /* qpsk.rs:15 */
+    p->bits_per_symbol = 2; return 0;
+}
+int or_qam_new(or_phasor* p, size_t bps, float phase, float amplitude) {    /* qam.rs:15-30 */
+    if (!(bps > 1)) return -1;                            /* qam.rs:17 */
+    or_phasor_zero(p, OR_QAM);
+    size_t cs = bps / 2;                                  /* qam.rs:19 */
+    float ms = (float)or_max_symbol(cs);                  /* qam.rs:20 */
+    p->bits_per_symbol = bps; p->bits_per_carrier = cs; p->max_symbol = ms;
+    p->phase_cos = cosf(phase); p->phase_sin = sinf(phase);
+    p->amplitude = amplitude / ms / 2.0f;                 /* qam.rs:28 */
+    return 0;
+}
+int or_bask_new(or_phasor* p, float amplitude) {                            /* bask.rs:8-12 */
+    or_phasor_zero(p, OR_BASK); p->amplitude = amplitude; p->bits_per_symbol = 1; return 0;
+}
+int or_mpsk_new(or_phasor* p, size_t bps, float phase_offset, float amplitude) { /* mpsk.rs:14-21 */
+    or_phasor_zero(p, OR_MPSK);
+    p->bits_per_symbol = bps; p->num_symbols = (float)((size_t)1 << bps);
+    p->amplitude = amplitude; p->phase = phase_offset; return 0;
+}
+int or_apsk_new(or_phasor* p, float amplitude, size_t bps, const or_ring* rings, int n) {
+    if (n < 1 || n > 8) return -1;
+    for (int k = 0; k < n; k++)                           /* Ring::new assert, apsk.rs:74 */
+        if (!(rings[k].radius >= 0.0f && rings[k].radius <= 1.0f)) return -1;
+    unsigned prev = 0;                                    /* verify(), apsk.rs:85-97 */
+    for (int k = 0; k < n; k++) { if (rings[k].start != prev) return -1; prev = rings[k].end; }
+    if ((size_t)prev != or_max_symbol(bps) + 1) return -1;    /* assert!, apsk.rs:26 */
+    or_phasor_zero(p, OR_APSK);
+    p->amplitude = amplitude; p->bits_per_symbol = bps; p->nrings = n;
+    memcpy(p->rings, rings, sizeof(or_ring) * (size_t)n);
+    return 0;
+}
+int or_oqpsk_new(or_phasor* p, float amplitude) {                           /* oqpsk.rs:9-13 */
+    or_phasor_zero(p, OR_OQPSK); p->amplitude = amplitude * sqrtf(0.5f);
+    p->bits_per_symbol = 2; return 0;
+}
+int or_dcqpsk_new(or_phasor* p, float amplitude) {                          /* dcqpsk.rs:16-21 */
+    or_phasor_zero(p, OR_DCQPSK); p->amplitude = amplitude; p->even = 0;
+    p->bits_per_symbol = 2; return 0;
+}
+int or_dmpsk_new(or_phasor* p, size_t bps, float amplitude, float phase, float shift) {
+    or_phasor_zero(p, OR_DMPSK);                                             /* dmpsk.rs:16-23 */
+    p->bits_per_symbol = bps; p->amplitude = amplitude; p->phase = phase; p->shift = shift;
+    return 0;
+}
+size_t or_phasor_bits_per_symbol(const or_phasor* p) { return p->bits_per_symbol; }
+
+static float or_qam_pos(const or_phasor* p, const uint8_t* b, size_t n) {   /* qam.rs:32-38 */
+    return 2.0f * (float)or_bytes_to_bits(b, n) - p->max_symbol;
+}
+static float or_apsk_common(const or_phasor* p, uint8_t symbol, float* radius) { /* apsk.rs:36-42 */
+    const or_ring* ring = NULL;
+    for (int k = 0; k < p->nrings; k++)
+        if (symbol >= p->rings[k].start && symbol < p->rings[k].end) { ring = &p->rings[k]; break; }
+    if (!ring) ring = &p->rings[0];                       /* unreachable after verify() */
+    *radius = ring->radius;
+    return 2.0f * OR_PI * (float)(uint8_t)(symbol - ring->start) /
+           (float)(uint8_t)(ring->end - ring->start) + ring->phase;
+}
+static float or_dcqpsk_term(const or_phasor* p, uint8_t symbol) {           /* dcqpsk.rs:23-36 */
+    const float MAP[4] = { 0.0f, OR_PI / 2.0f, 3.0f * OR_PI / 2.0f, OR_PI };
+    return p->even ? MAP[symbol & 3] + OR_PI / 4.0f : MAP[symbol & 3];
+}
+
+void or_phasor_update(or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
+    (void)s;
+    if (p->kind == OR_DCQPSK) p->even = !p->even;         /* dcqpsk.rs:42-44 */
+    else if (p->kind == OR_DMPSK)                         /* dmpsk.rs:29-33 */
+        p->phase = or_mod_trig(p->phase + (float)or_bytes_to_bits(b, n) * p->shift);
+}
+
+float or_phasor_i(const or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
+    (void)s;
+    switch (p->kind) {
+    case OR_BPSK: return (or_bit_to_sign(b[0]) * p->amplitude) * cosf(p->phase); /* bpsk.rs:17-27 */
+    case OR_QPSK: return p->amplitude * (or_bit_to_sign(b[0]) * p->phase_cos -
+                                         or_bit_to_sign(b[1]) * p->phase_sin); /* qpsk.rs:23-28 */
+    case OR_QAM: {                                                             /* qam.rs:44-51 */
+        size_t cs = p->bits_per_carrier;
+        return p->amplitude * (or_qam_pos(p, b, cs) * p->phase_cos -
+                               or_qam_pos(p, b + cs, n - cs) * p->phase_sin);
+    }
+    case OR_BASK: return (float)b[0] * p->amplitude;                           /* bask.rs:18-20 */
+    case OR_MPSK: {                                                            /* mpsk.rs:23-37 */
+        float ph = 2.0f * OR_PI * (float)or_bytes_to_bits(b, n) / p->num_symbols;
+        return p->amplitude * cosf(ph + p->phase);
+    }
+    case OR_APSK: { float r; float in = or_apsk_common(p, or_bytes_to_bits(b, n), &r);
+                    return p->amplitude * r * cosf(in); }                      /* apsk.rs:48-51 */
+    case OR_OQPSK: return or_bit_to_sign(b[0]) * p->amplitude;                 /* oqpsk.rs:19-21 */
+    case OR_DCQPSK: return p->amplitude * cosf(or_dcqpsk_term(p, or_bytes_to_bits(b, n))); /* dcqpsk.rs:46-48 */
+    case OR_DMPSK: return p->amplitude * cosf(p->phase);                       /* dmpsk.rs:35-37 */
+    }
+    return 0.0f;
+}
+float or_phasor_q(const or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
+    (void)s;
+    switch (p->kind) {
+    case OR_BPSK: return (or_bit_to_sign(b[0]) * p->amplitude) * sinf(p->phase); /* bpsk.rs:29-31 */
+    case OR_QPSK: return p->amplitude * (or_bit_to_sign(b[1]) * p->phase_cos +
+                                         or_bit_to_sign(b[0]) * p->phase_sin); /* qpsk.rs:30-35 */
+    case OR_QAM: {                                                             /* qam.rs:53-60 */
+        size_t cs = p->bits_per_carrier;
+        return p->amplitude * (or_qam_pos(p, b + cs, n - cs) * p->phase_cos +
+                               or_qam_pos(p, b, cs) * p->phase_sin);
+    }
+    case OR_BASK: return 0.0f;                                                 /* bask.rs:22-24 */
+    case OR_MPSK: {                                                            /* mpsk.rs:39-41 */
+        float ph = 2.0f * OR_PI * (float)or_bytes_to_bits(b, n) / p->num_symbols;
+        return p->amplitude * sinf(ph + p->phase);
+    }
+    case OR_APSK: { float r; float in = or_apsk_common(p, or_bytes_to_bits(b, n), &r);
+                    return p->amplitude * r * sinf(in); }                      /* apsk.rs:53-56 */
+    case OR_OQPSK: return or_bit_to_sign(b[1]) * p->amplitude;                 /* oqpsk.rs:23-25 */
+    case OR_DCQPSK: return p->amplitude * sinf(or_dcqpsk_term(p, or_bytes_to_bits(b, n))); /* dcqpsk.rs:50-52 */
+    case OR_DMPSK: return p->amplitude * sinf(p->phase);                       /* dmpsk.rs:39-41 */
+    }
+    return 0.0f;
+}
+
+/* ---- fir.rs ------------------------------------------------------------------------------ */
+int or_fir_init(or_fir* f, const float* coefs, size_t len) {                 /* fir.rs:10-16 */
+    f->coefs = coefs; f->len = len; f->idx = 0;
+    f->history = (float*)calloc(len ? len : 1, sizeof(float));
+    return f->history ? 0 : -1;
+}
+void or_fir_free(or_fir* f) { free(f->history); f->history = NULL; }
+float or_fir_calc(const or_fir* f) {                                         /* fir.rs:18-25 */
+    size_t cur = f->idx;
+    float s = 0.0f;
+    for (size_t k = 0; k < f->len; k++) {
+        size_t m = cur - 1;                               /* usize wraps in --release */
+        cur = m < f->len - 1 ? m : f->len - 1;            /* cmp::min(cur - 1, len - 1) */
+        s = s + f->history[cur] * f->coefs[k];
+    }
+    return s;
+}
+float or_fir_add(or_fir* f, float sample) {                                  /* fir.rs:27-34 */
+    f->history[f->idx] = sample;
+    f->idx += 1;
+    f->idx %= f->len;
+    return or_fir_calc(f);
+}
+void or_fir_block(const float* coefs, size_t len, const float* in, size_t n, float* out) {
+    or_fir f; if (or_fir_init(&f, coefs, len)) return;
+    for (size_t i = 0; i < n; i++) out[i] = or_fir_add(&f, in[i]);
+    or_fir_free(&f);
+}
+
+/* ---- modulator.rs ------------------------------------------------------------------------ */
+float or_iq_real(const or_iq_sample* s, float c, float sn) { return s->i * c - s->q * sn; } /* :37-39 */
+float or_iq_imag(const or_iq_sample* s, float c, float sn) { return s->i * sn + s->q * c; } /* :41-43 */
+void or_iq_modulate(const or_iq_sample* s, float* re, float* im) {           /* modulator.rs:45-48 */
+    float sn = sinf(s->carrier), c = cosf(s->carrier);   /* f32::sin_cos */
+    *re = or_iq_real(s, c, sn);
+    *im = or_iq_imag(s, c, sn);
+}
+
+/* DigitalModulator::next (modulator.rs:85-100) over any Source. Returns 0 at Finished. */
+static int or_dm_next(or_carrier* c, or_phasor* p, int (*src_next)(void*, const uint8_t**),
+                      void* src, or_iq_sample* out, int* changed) {
+    float phase = or_carrier_next(c);                     /* :86 */
+    const uint8_t* bits = NULL;
+    int u = src_next(src, &bits);                         /* :88 */
+    if (u == OR_FINISHED) return 0;                       /* :89 */
+    size_t n = p->bits_per_symbol;
+    if (u == OR_CHANGED) or_phasor_update(p, c->sample, bits, n);  /* :90-93 */
+    out->carrier = phase;                                 /* :97-99 */
+    out->i = or_phasor_i(p, c->sample, bits, n);
+    out->q = or_phasor_q(p, c->sample, bits, n);
+    *changed = (u == OR_CHANGED);
+    return 1;
+}
+static int or_bits_next_v(void* s, const uint8_t** b) { return or_bits_next((or_bits_source*)s, b); }
+static int or_source_next_v(void* s, const uint8_t** b) { return or_source_next((or_source*)s, b); }
+static int or_even_odd_next_v(void* s, const uint8_t** b) { return or_even_odd_next((or_even_odd*)s, b); }
+
+size_t or_digital_modulate(or_carrier* c, or_phasor* p, const uint8_t* bits, size_t nbits,
+                           size_t sps, or_iq_sample* out, uint8_t* changed, size_t cap) {
+    or_bits_source src; or_bits_init(&src, bits, nbits, sps, p->bits_per_symbol);
+    size_t k = 0;
+    while (k < cap) {
+        int ch;
+        if (!or_dm_next(c, p, or_bits_next_v, &src, &out[k], &ch)) break;
+        if (changed) changed[k] = (uint8_t)ch;
+        k++;
+    }
+    return k;
+}
+
+/* ---- pll.rs / demodulator.rs -------------------------------------------------------------- */
+void or_pll_handle(or_pll* p, float carrier_phase, float xr, float xi) {     /* pll.rs:16-22 */
+    const float CHANGE = 0.447214f;                       /* pll.rs:3 */
+    float inner = carrier_phase + p->phase_offset;
+    float cr = cosf(inner), ci = -sinf(inner);            /* Complex::new(cos, sin).conj() */
+    float re = xr * cr - xi * ci;                         /* num::Complex Mul */
+    float im = xr * ci + xi * cr;
+    float err = atan2f(im, re);                           /* Complex::arg */
+    p->phase_offset += CHANGE * err;
+}
+void or_demodulate(float sf, uint64_t s0, float phase_offset, const float* taps, size_t ntaps,
+                   const float* x_re, size_t n, float* out_i, float* out_q) {
+    or_carrier c; or_carrier_init(&c, sf, s0);           /* demodulator.rs:20-30 */
+    or_fir lpi, lpq; or_fir_init(&lpi, taps, ntaps); or_fir_init(&lpq, taps, ntaps);
+    for (size_t k = 0; k < n; k++) {                      /* demodulator.rs:44-56 */
+        float x = x_re[k];
+        float phase = or_carrier_next(&c) + phase_offset;
+        out_i[k] = 2.0f * or_fir_add(&lpi, x * cosf(phase));
+        out_q[k] = 2.0f * or_fir_add(&lpq, x * -sinf(phase));
+    }
+    or_fir_free(&lpi); or_fir_free(&lpq);
+}
+
+/* ---- GLUE ----------------------------------------------------------------------------------- */
+uint64_t or_splitmix64_next(uint64_t* state) {
+    uint64_t z = (*state += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+void or_prng_bits(uint64_t seed, uint8_t* out, size_t nbits) {
+    uint64_t st = seed, w = 0;
+    for (size_t i = 0; i < nbits; i++) {
+        if ((i & 63) == 0) w = or_splitmix64_next(&st);
+        out[i] = (uint8_t)((w >> (i & 63)) & 1);
+    }
+}
+
+int or_rrc_taps(size_t L, size_t sps, double beta, float* out) {
+    if (L == 0 || sps == 0 || beta < 0.0 || beta > 1.0) return -1;
+    const double pi = 3.14159265358979323846;
+    double* h = (double*)malloc(L * sizeof(double));
+    if (!h) return -1;
+    double e = 0.0;
+    for (size_t i = 0; i < L; i++) {
+        double t = ((double)i - (double)(L - 1) / 2.0) / (double)sps;
+        double v;
+        if (t == 0.0) v = 1.0 - beta + 4.0 * beta / pi;
+        else if (beta > 0.0 && fabs(fabs(4.0 * beta * t) - 1.0) < 1e-12)
+            v = beta / sqrt(2.0) * ((1.0 + 2.0 / pi) * sin(pi / (4.0 * beta)) +
+                                    (1.0 - 2.0 / pi) * cos(pi / (4.0 * beta)));
+        else
+            v = (sin(pi * t * (1.0 - beta)) + 4.0 * beta * t * cos(pi * t * (1.0 + beta))) /
+                (pi * t * (1.0 - (4.0 * beta * t) * (4.0 * beta * t)));
+        h[i] = v; e += v * v;
+    }
+    double g = 1.0 / sqrt(e);
+    for (size_t i = 0; i < L; i++) out[i] = (float)(h[i] * g);
+    free(h);
+    return 0;
+}
+
+int or_phasor_lut(const or_phasor* p, float* lut) {
+    size_t bps = p->bits_per_symbol;
+    if (bps < 1 || bps > 8) return -1;
+    uint8_t b[8];
+    for (size_t s = 0; s < ((size_t)1 << bps); s++) {
+        for (size_t k = 0; k < bps; k++) b[k] = (uint8_t)((s >> (bps - 1 - k)) & 1); /* MSB first */
+        lut[2 * s] = or_phasor_i(p, 0, b, bps);           /* phasor.rs:9-11 */
+        lut[2 * s + 1] = or_phasor_q(p, 0, b, bps);
+    }
+    return 0;
+}
+
+uint8_t or_slice(const or_slicer* s, float re, float im) {
+    if (s->kind == OR_SLICER_QAM_AXIS) {
+        int ms = (int)s->max_symbol;
+        float fi = (re * s->inv_scale + s->max_symbol) * 0.5f;
+        float fq = (im * s->inv_scale + s->max_symbol) * 0.5f;
+        int si = (int)rintf(fi), sq = (int)rintf(fq);
+        si = si < 0 ? 0 : (si > ms ? ms : si);
+        sq = sq < 0 ? 0 : (sq > ms ? ms : sq);
+        return (uint8_t)((si << s->bits_per_carrier) | sq);
+    }
+    size_t n = (size_t)1 << s->bps;
+    uint8_t best = 0; float bd = INFINITY;
+    for (size_t k = 0; k < n; k++) {
+        float dr = re - s->lut[2 * k], di = im - s->lut[2 * k + 1];
+        float d = dr * dr + di * di;
+        if (d < bd) { bd = d; best = (uint8_t)k; }
+    }
+    return best;
+}
+
+size_t or_tx_chain(or_phasor* p, const uint8_t* bits, size_t nbits, size_t sps,
+                   const float* taps, size_t ntaps, float sf, uint64_t s0,
+                   size_t flush_syms, int out_mode, float* out) {
+    or_carrier c; or_carrier_init(&c, sf, s0);
+    or_bits_source src; or_bits_init(&src, bits, nbits, sps, p->bits_per_symbol);
+    or_fir fi, fq;
+    if (ntaps) { or_fir_init(&fi, taps, ntaps); or_fir_init(&fq, taps, ntaps); }
+    size_t k = 0, nflush = flush_syms * sps;
+    int finished = 0;
+    for (;;) {
+        or_iq_sample s; int changed = 0;
+        if (!finished) {
+            or_carrier saved = c;
+            if (!or_dm_next(&c, p, or_bits_next_v, &src, &s, &changed)) {
+                finished = 1; c = saved;      /* the Finished call's carrier tick is not a sample */
+            }
+        }
+        if (finished) {                        /* GLUE: flush = zero symbols, carrier runs on */
+            if (nflush == 0) break;
+            nflush--;
+            s.carrier = or_carrier_next(&c); s.i = 0.0f; s.q = 0.0f; changed = 0;
+        }
+        float xi = s.i, xq = s.q;
+        if (ntaps) {                           /* GLUE: zero-stuff (impulse at the symbol tick) */
+            if (!changed) { xi = 0.0f; xq = 0.0f; }
+            xi = or_fir_add(&fi, xi);          /* fir.rs:27-34, one filter per rail */
+            xq = or_fir_add(&fq, xq);
+        }
+        or_iq_sample y = { s.carrier, xi, xq };
+        if (out_mode == OR_OUT_IQ_BASEBAND) { out[2 * k] = xi; out[2 * k + 1] = xq; }
+        else {
+            float re, im; or_iq_modulate(&y, &re, &im);   /* modulator.rs:45-48 */
+            if (out_mode == OR_OUT_REAL) out[k] = re;
+            else { out[2 * k] = re; out[2 * k + 1] = im; }
+        }
+        k++;
+    }
+    if (ntaps) { or_fir_free(&fi); or_fir_free(&fq); }
+    return k;
+}
+
+size_t or_rx_chain(const float* x, size_t n, float sf, uint64_t s0, int mix,
+                   const float* taps, size_t ntaps, size_t sps, size_t D,
+                   const or_slicer* slicer, float* out_iq, uint8_t* out_sym, size_t cap) {
+    or_carrier c; or_carrier_init(&c, sf, s0);
+    const float phase_offset = 0.0f;                      /* PLL not locked (demodulator.rs:50) */
+    or_fir lpi, lpq; or_fir_init(&lpi, taps, ntaps); or_fir_init(&lpq, taps, ntaps);
+    size_t nsym = 0;
+    for (size_t k = 0; k < n; k++) {
+        float xr = x[2 * k], xi = x[2 * k + 1];
+        float phase = or_carrier_next(&c) + phase_offset;
+        float zr, zi;
+        if (mix == OR_MIX_REFERENCE_REAL) {               /* demodulator.rs:46,53-54 */
+            zr = xr * cosf(phase); zi = xr * -sinf(phase);
+        } else {                                          /* GLUE: x * conj(e^{j phase}) */
+            float cs = cosf(phase), sn = sinf(phase);
+            zr = xr * cs + xi * sn; zi = xi * cs - xr * sn;
+        }
+        float ri = or_fir_add(&lpi, zr), rq = or_fir_add(&lpq, zi);
+        if (mix == OR_MIX_REFERENCE_REAL) { ri = 2.0f * ri; rq = 2.0f * rq; }  /* :53-54 */
+        if (k >= D && (k - D) % sps == 0 && nsym < cap) { /* GLUE: decimate */
+            if (out_iq) { out_iq[2 * nsym] = ri; out_iq[2 * nsym + 1] = rq; }
+            if (out_sym && slicer) out_sym[nsym] = or_slice(slicer, ri, rq);
+            nsym++;
+        }
+    }
+    or_fir_free(&lpi); or_fir_free(&lpq);
+    return nsym;
+}
+
+/* ---- bin/modulate.rs:20-134 ------------------------------------------------------------------ */
+long or_modulate_cli(const char* name, size_t sr, size_t br, size_t cf, size_t pc, int iq,
+                     const char* text, size_t len, float* out, size_t cap) {
+    const float AMPLITUDE = 1.0f;                         /* modulate.rs:14 */
+    if (pc > 0 && sr % cf != 0) return -1;                /* :62 */
+    if (!(cf < sr / 2)) return -1;                        /* :68 */
+    size_t sps = or_rates_samples_per_symbol(br, sr);     /* :70 */
+    or_carrier carrier; or_carrier_init(&carrier, or_freq_sample_freq(cf, sr), 0);  /* :71 */
+    or_phasor p;                                          /* :74-95 */
+    if (!strcmp(name, "bask")) or_bask_new(&p, AMPLITUDE);
+    else if (!strcmp(name, "bpsk")) or_bpsk_new(&p, OR_PI / 4.0f, AMPLITUDE);
+    else if (!strcmp(name, "qpsk")) or_qpsk_new(&p, 0.0f, AMPLITUDE);
+    else if (!strcmp(name, "qam16")) or_qam_new(&p, 4, 0.0f, AMPLITUDE);
+    else if (!strcmp(name, "qam256")) or_qam_new(&p, 8, 0.0f, AMPLITUDE);
+    else if (!strcmp(name, "16psk")) or_mpsk_new(&p, 4, 0.0f, AMPLITUDE);
+    else if (!strcmp(name, "oqpsk")) or_oqpsk_new(&p, AMPLITUDE);
+    else if (!strcmp(name, "dcqpsk")) or_dcqpsk_new(&p, AMPLITUDE);
+    else if (!strcmp(name, "16apsk")) {
+        or_ring r[2] = { { 0, 4, 0.5f, OR_PI / 4.0f }, { 4, 16, 1.0f, OR_PI / 12.0f } };
+        if (or_apsk_new(&p, AMPLITUDE, 4, r, 2)) return -1;
+    }
+    else if (!strcmp(name, "dqpsk")) or_dmpsk_new(&p, 2, AMPLITUDE, OR_PI / 4.0f, OR_PI / 2.0f);
+    else if (!strcmp(name, "dbpsk")) or_dmpsk_new(&p, 1, AMPLITUDE, OR_PI / 4.0f, OR_PI);
+    else return -2;                                       /* bfsk/msk/mfsk/16cpfsk: out of scope */
+
+    or_source bits; memset(&bits, 0, sizeof bits);        /* :98-99 */
+    bits.is_ascii = 1; or_ascii_init(&bits.ascii, text, len, sps, p.bits_per_symbol);
+    or_even_odd eo;
+    void* src = &bits; int (*next)(void*, const uint8_t**) = or_source_next_v;
+    if (!strcmp(name, "oqpsk")) {                         /* :101-107 */
+        if (or_even_odd_init(&eo, &bits, sps, p.bits_per_symbol)) return -1;
+        src = &eo; next = or_even_odd_next_v;
+    }
+    size_t k = 0;
+    or_iq_sample s; int ch;
+    if (iq) {                                             /* :109-116 */
+        while (or_dm_next(&carrier, &p, next, src, &s, &ch)) {
+            if (k + 2 > cap) return -1;
+            out[k++] = s.i; out[k++] = s.q;
+        }
+    } else {
+        if (pc > 0) {                                     /* :118-126 preamble, Raw phasor */
+            size_t nt = sr / cf * pc - 1;
+            for (size_t t = 0; t < nt; t++) {
+                or_iq_sample pre = { or_carrier_next(&carrier), AMPLITUDE, 0.0f };
+                float re, im; or_iq_modulate(&pre, &re, &im);
+                if (k + 1 > cap) return -1;
+                out[k++] = re;
+            }
+        }
+        while (or_dm_next(&carrier, &p, next, src, &s, &ch)) {   /* :128-133 */
+            float re, im; or_iq_modulate(&s, &re, &im);
+            if (k + 1 > cap) return -1;
+            out[k++] = re;
+        }
+    }
+    if (bits.ascii.panicked || (src == &eo && eo.data.ascii.panicked)) return -1;
+    return (long)k;
+}

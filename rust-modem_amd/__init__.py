@@ -1,0 +1,586 @@
+"""rust_modem_amd — Python mirror of ramtej/rust-modem's modem API over the gfx950 backend.
+
+The product is `lib/libmodem_hip.so` (HIP kernels + the C ABI of include/modem_hip.h); this
+module is a thin ctypes layer that keeps the reference crate's names and argument meanings
+so callers (and the parity tests) read like the reference:
+
+    reference (src/modem)                          here
+    Freq::new(hz, sr).sample_freq()  freq.rs:19-26  Freq(hz, sr).sample_freq()
+    Rates::new(br, sr)               rates.rs:12-18 Rates(br, sr).samples_per_symbol
+    Carrier::new(freq), .sample      carrier.rs:4-26 Carrier(freq), .sample, .next()
+    BPSK/QPSK/QAM/BASK/MPSK/APSK/OQPSK digital/*.rs BPSK(...)... (.i/.q/.bits_per_symbol)
+    DigitalModulator::new(&mut c, phasor, src)      DigitalModulator(carrier, phasor, sps, taps)
+        modulator.rs:64-101                             .process(bits) -> samples (device)
+    FIRFilter::new(&taps).add(x)     fir.rs:3-35    FIRFilter(taps).add(x) / .process(block)
+    Demodulator::new(c, sig, lp)     demodulator.rs DemodulatorRx(carrier, taps, ...)
+                                                        .process(iq) -> (decimated iq, symbols)
+
+Where the reference panics (assert!, unwrap, index out of range) this layer raises
+`ModemPanic`. The HIP library is required: importing works without a GPU (host-only
+entry points such as the LUT builders run on the CPU), but every device entry point raises
+if the library is missing or no gfx950 device is present — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+__all__ = [
+    "ModemPanic", "ModemError", "lib_path", "load_library",
+    "Freq", "Rates", "Carrier", "Ring",
+    "BPSK", "QPSK", "QAM", "BASK", "MPSK", "APSK", "OQPSK",
+    "rrc_taps", "DigitalModulator", "DemodulatorRx", "FIRFilter", "prng_bits",
+    "MIX_COMPLEX", "MIX_REFERENCE_REAL", "OUT_IQ_MIXED", "OUT_IQ_BASEBAND", "OUT_REAL",
+    "SLICER_NONE", "SLICER_NEAREST", "SLICER_QAM_AXIS", "DTYPE_F32", "DTYPE_F16",
+]
+
+PI32 = float(np.float32(math.pi))      # std::f32::consts::PI
+
+MODEM_OK, ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_DEVICE, ERR_CAPACITY, ERR_ALLOC = (
+    0, -1, -2, -3, -4, -5, -6)
+DTYPE_F32, DTYPE_F16 = 0, 1
+OUT_IQ_MIXED, OUT_IQ_BASEBAND, OUT_REAL = 0, 1, 2
+MIX_COMPLEX, MIX_REFERENCE_REAL = 0, 1
+SLICER_NONE, SLICER_NEAREST, SLICER_QAM_AXIS = 0, 1, 2
+_PH_BPSK, _PH_QPSK, _PH_QAM, _PH_BASK, _PH_MPSK, _PH_APSK, _PH_OQPSK = 1, 2, 3, 4, 5, 6, 7
+
+
+class ModemError(RuntimeError):
+    """A backend failure (HIP error, no device, capacity)."""
+
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"{what}: {status_str(status)} ({status})" if what else status_str(status))
+
+
+class ModemPanic(ModemError):
+    """Raised where the reference crate would panic (assert!/unwrap/index)."""
+
+
+# ------------------------------------------------------------------------- library ----
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def lib_path() -> str:
+    return os.path.join(_HERE, "lib", "libmodem_hip.so")
+
+
+class _Ring(ctypes.Structure):
+    _fields_ = [("start", ctypes.c_uint8), ("end", ctypes.c_uint8),
+                ("radius", ctypes.c_float), ("phase", ctypes.c_float)]
+
+
+class _PhasorDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("bits_per_symbol", ctypes.c_uint32),
+                ("phase", ctypes.c_float), ("amplitude", ctypes.c_float),
+                ("nrings", ctypes.c_uint32), ("rings", ctypes.POINTER(_Ring))]
+
+
+class _SlicerDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("bits_per_symbol", ctypes.c_uint32),
+                ("lut", ctypes.POINTER(ctypes.c_float)), ("bits_per_carrier", ctypes.c_uint32),
+                ("inv_scale", ctypes.c_float), ("max_symbol", ctypes.c_float)]
+
+
+class _TxDesc(ctypes.Structure):
+    _fields_ = [("bits_per_symbol", ctypes.c_uint32), ("lut", ctypes.POINTER(ctypes.c_float)),
+                ("samples_per_symbol", ctypes.c_uint32), ("taps", ctypes.POINTER(ctypes.c_float)),
+                ("ntaps", ctypes.c_uint32), ("sample_freq", ctypes.c_float),
+                ("s0", ctypes.c_uint64), ("dtype", ctypes.c_int32), ("out_mode", ctypes.c_int32)]
+
+
+class _RxDesc(ctypes.Structure):
+    _fields_ = [("sample_freq", ctypes.c_float), ("s0", ctypes.c_uint64),
+                ("taps", ctypes.POINTER(ctypes.c_float)), ("ntaps", ctypes.c_uint32),
+                ("decim", ctypes.c_uint32), ("decim_offset", ctypes.c_uint32),
+                ("mix", ctypes.c_int32), ("in_dtype", ctypes.c_int32),
+                ("out_dtype", ctypes.c_int32), ("slicer", _SlicerDesc)]
+
+
+_lib = None
+_lib_err: Optional[str] = None
+
+
+def load_library():
+    """Load lib/libmodem_hip.so (raises if it was not built)."""
+    global _lib, _lib_err
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        _lib_err = f"{path} not built (run __graft_entry__.build() or `make -C rust-modem_amd`)"
+        raise ModemError(ERR_UNSUPPORTED, _lib_err)
+    L = ctypes.CDLL(path)
+    c = ctypes
+    vp, sz, u64, u32, f32, st = c.c_void_p, c.c_size_t, c.c_uint64, c.c_uint32, c.c_float, c.c_int
+    fp = c.POINTER(c.c_float)
+    sig = {
+        "modem_status_str": (c.c_char_p, [st]),
+        "modem_abi_version": (c.c_int32, []),
+        "modem_freq_sample_freq": (f32, [u64, u64]),
+        "modem_rates_sps": (st, [u64, u64, c.POINTER(u64)]),
+        "modem_carrier_phase": (f32, [f32, u64]),
+        "modem_carrier_phases": (st, [f32, u64, sz, vp, c.c_int, vp]),
+        "modem_phasor_bits": (st, [c.POINTER(_PhasorDesc), c.POINTER(u32)]),
+        "modem_phasor_lut": (st, [c.POINTER(_PhasorDesc), fp]),
+        "modem_phasor_slicer": (st, [c.POINTER(_PhasorDesc), fp, c.POINTER(_SlicerDesc)]),
+        "modem_rrc_taps": (st, [u32, u32, c.c_double, fp]),
+        "modem_tx_create": (st, [c.POINTER(_TxDesc), c.c_int, c.POINTER(vp)]),
+        "modem_tx_process": (st, [vp, vp, sz, vp, sz, c.POINTER(sz), vp]),
+        "modem_tx_flush": (st, [vp, vp, sz, c.POINTER(sz), vp]),
+        "modem_tx_sample": (u64, [vp]),
+        "modem_tx_destroy": (st, [vp]),
+        "modem_rx_create": (st, [c.POINTER(_RxDesc), c.c_int, c.POINTER(vp)]),
+        "modem_rx_process": (st, [vp, vp, sz, vp, vp, sz, c.POINTER(sz), vp]),
+        "modem_rx_flush": (st, [vp, vp, vp, sz, c.POINTER(sz), vp]),
+        "modem_rx_sample": (u64, [vp]),
+        "modem_rx_destroy": (st, [vp]),
+        "modem_fir_create": (st, [fp, u32, c.c_int, c.POINTER(vp)]),
+        "modem_fir_process": (st, [vp, vp, vp, sz, vp]),
+        "modem_fir_destroy": (st, [vp]),
+        "modem_prng_bits": (st, [u64, vp, sz, c.c_int, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    _lib = L
+    return L
+
+
+def status_str(s: int) -> str:
+    try:
+        return load_library().modem_status_str(s).decode()
+    except ModemError:
+        return f"status {s}"
+
+
+def _check(status: int, what: str):
+    if status == MODEM_OK:
+        return
+    if status == ERR_INVALID_ARG:
+        raise ModemPanic(status, what)
+    raise ModemError(status, what)
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+
+
+# --------------------------------------------------------------- timebase (B4) ----
+class Freq:
+    """freq.rs:3-27 — cycles per second at a sample rate."""
+
+    def __init__(self, hz: int, sr: int):
+        self.hz, self.sr = int(hz), int(sr)
+
+    def ang_freq(self) -> float:
+        return float(np.float32(2.0) * np.float32(PI32) * np.float32(self.hz))
+
+    def sample_freq(self) -> float:
+        return float(load_library().modem_freq_sample_freq(self.hz, self.sr))
+
+
+class Rates:
+    """rates.rs:1-19 — samples_per_symbol = sr / br (integer division)."""
+
+    def __init__(self, br: int, sr: int):
+        if br == 0:
+            raise ModemPanic(ERR_INVALID_ARG, "Rates::new: attempt to divide by zero")
+        self.baud_rate, self.sample_rate = int(br), int(sr)
+        self.samples_per_symbol = int(sr) // int(br)
+
+
+class Carrier:
+    """carrier.rs:3-27 — phase(n) = mod_trig(sample_freq * (n as f32)); `sample` is the next n."""
+
+    def __init__(self, freq: Freq, sample: int = 0):
+        self.sample_freq = freq.sample_freq() if isinstance(freq, Freq) else float(freq)
+        self.sample = int(sample)
+
+    def inner(self, s: int) -> float:
+        return float(load_library().modem_carrier_phase(self.sample_freq, int(s)))
+
+    def next(self) -> float:
+        s = self.sample
+        self.sample += 1
+        return self.inner(s)
+
+    def phases(self, s0: int, n: int, device: int = 0, stream=None):
+        """inner(s0 .. s0+n-1) on the device (the kernels' phase code path), a CUDA tensor."""
+        import torch
+        out = torch.empty(int(n), dtype=torch.float32, device=f"cuda:{device}")
+        _check(load_library().modem_carrier_phases(self.sample_freq, int(s0), int(n),
+                                                   out.data_ptr() if n else None, device,
+                                                   _stream_handle(stream)), "Carrier.phases")
+        return out
+
+
+# ------------------------------------------------------------ DigitalPhasor (B2) ----
+class _Phasor:
+    """Memoryless DigitalPhasor (digital/phasor.rs:1-12) as a host-built (I,Q) table."""
+
+    _kind = 0
+
+    def _desc(self) -> _PhasorDesc:
+        d = _PhasorDesc()
+        d.kind = self._kind
+        d.bits_per_symbol = getattr(self, "_bps", 0)
+        d.phase = getattr(self, "_phase", 0.0)
+        d.amplitude = self.amplitude
+        d.nrings = 0
+        return d
+
+    def bits_per_symbol(self) -> int:
+        b = ctypes.c_uint32()
+        _check(load_library().modem_phasor_bits(ctypes.byref(self._desc()), ctypes.byref(b)),
+               type(self).__name__)
+        return int(b.value)
+
+    def lut(self) -> np.ndarray:
+        """(2^bps, 2) float32: row s = (i, q) of the bits of s, MSB first."""
+        n = 1 << self.bits_per_symbol()
+        out = np.zeros((n, 2), dtype=np.float32)
+        _check(load_library().modem_phasor_lut(ctypes.byref(self._desc()), _fptr(out)),
+               type(self).__name__)
+        return out
+
+    def _index(self, b: Sequence[int]) -> int:
+        s = 0
+        for v in b:
+            s = (s << 1) | (int(v) & 1)   # bytes_to_bits, digital/util.rs:5-11
+        return s
+
+    def i(self, s: int, b: Sequence[int]) -> float:
+        return float(self.lut()[self._index(b), 0])
+
+    def q(self, s: int, b: Sequence[int]) -> float:
+        return float(self.lut()[self._index(b), 1])
+
+    def next(self, s: int, b: Sequence[int]) -> Tuple[float, float]:
+        return self.i(s, b), self.q(s, b)
+
+    def slicer(self) -> _SlicerDesc:
+        lut = self.lut()
+        self._slicer_lut = lut          # keep alive until handed to a handle
+        sd = _SlicerDesc()
+        _check(load_library().modem_phasor_slicer(ctypes.byref(self._desc()), _fptr(lut),
+                                                  ctypes.byref(sd)), "slicer")
+        return sd
+
+
+class BPSK(_Phasor):
+    """bpsk.rs:4-32."""
+    _kind = _PH_BPSK
+
+    def __init__(self, phase: float, amplitude: float):
+        self._phase, self.amplitude = float(phase), float(amplitude)
+
+
+class QPSK(_Phasor):
+    """qpsk.rs:4-36."""
+    _kind = _PH_QPSK
+
+    def __init__(self, phase: float, amplitude: float):
+        self._phase, self.amplitude = float(phase), float(amplitude)
+
+
+class QAM(_Phasor):
+    """qam.rs:4-61 (natural-binary per axis; I from the MSB half)."""
+    _kind = _PH_QAM
+
+    def __init__(self, bits_per_symbol: int, phase: float, amplitude: float):
+        if not bits_per_symbol > 1:
+            raise ModemPanic(ERR_INVALID_ARG, "QAM::new: assertion failed: bits_per_symbol > 1")
+        self._bps, self._phase, self.amplitude = int(bits_per_symbol), float(phase), float(amplitude)
+
+
+class BASK(_Phasor):
+    """bask.rs:3-25."""
+    _kind = _PH_BASK
+
+    def __init__(self, a: float):
+        self.amplitude = float(a)
+
+
+class MPSK(_Phasor):
+    """mpsk.rs:6-42."""
+    _kind = _PH_MPSK
+
+    def __init__(self, bits_per_symbol: int, phase_offset: float, amplitude: float):
+        self._bps, self._phase, self.amplitude = int(bits_per_symbol), float(phase_offset), float(amplitude)
+
+
+class OQPSK(_Phasor):
+    """oqpsk.rs:4-26 (the symbol map; the half-symbol Q offset source is not on the GPU path)."""
+    _kind = _PH_OQPSK
+
+    def __init__(self, amplitude: float):
+        self.amplitude = float(amplitude)
+
+
+class Ring:
+    """apsk.rs:60-82."""
+
+    def __init__(self, rng: range, radius: float, phase: float):
+        if not (0.0 <= radius <= 1.0):
+            raise ModemPanic(ERR_INVALID_ARG, "Ring::new: assertion failed: radius in [0, 1]")
+        self.range, self.radius, self.phase = rng, float(radius), float(phase)
+
+
+class APSK(_Phasor):
+    """apsk.rs:12-57."""
+    _kind = _PH_APSK
+
+    def __init__(self, amplitude: float, bits_per_symbol: int, rings: Sequence[Ring]):
+        self.amplitude, self._bps, self.rings = float(amplitude), int(bits_per_symbol), list(rings)
+        self.lut()   # verify() (apsk.rs:26) raises ModemPanic on bad rings
+
+    def _desc(self):
+        d = super()._desc()
+        arr = (_Ring * len(self.rings))()
+        for k, r in enumerate(self.rings):
+            arr[k].start, arr[k].end = r.range.start, r.range.stop
+            arr[k].radius, arr[k].phase = r.radius, r.phase
+        self._rings_c = arr
+        d.nrings = len(self.rings)
+        d.rings = ctypes.cast(arr, ctypes.POINTER(_Ring))
+        return d
+
+
+def rrc_taps(ntaps: int, sps: int, beta: float = 0.35) -> np.ndarray:
+    """Root-raised-cosine taps (GLUE: absent from the reference), unit energy."""
+    out = np.zeros(int(ntaps), dtype=np.float32)
+    _check(load_library().modem_rrc_taps(int(ntaps), int(sps), float(beta), _fptr(out)), "rrc_taps")
+    return out
+
+
+# ------------------------------------------------------------- buffers / streams ----
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is not None:
+        return int(getattr(stream, "cuda_stream", stream))
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return int(torch.cuda.current_stream().cuda_stream)
+    except ImportError:
+        pass
+    return None
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if _is_torch(x):
+        if not x.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+        return int(x.data_ptr())
+    if not x.flags["C_CONTIGUOUS"]:
+        raise ValueError("array must be C-contiguous")
+    return int(x.ctypes.data)
+
+
+def _empty_like_input(ref, shape, np_dtype):
+    """Allocate an output on the same side (device tensor / host ndarray) as `ref`."""
+    if _is_torch(ref):
+        import torch
+        tdt = {np.float32: torch.float32, np.float16: torch.float16, np.uint8: torch.uint8}[np_dtype]
+        return torch.empty(shape, dtype=tdt, device=ref.device)
+    return np.empty(shape, dtype=np_dtype)
+
+
+def _device_of(x, default: int) -> int:
+    if _is_torch(x) and x.is_cuda:
+        return int(x.device.index or 0)
+    return default
+
+
+# ------------------------------------------------------------------- TX (B3+B5) ----
+class DigitalModulator:
+    """DigitalModulator (modulator.rs:64-101) + pulse shaping + IQSample::modulate.
+
+    `process(bits)` takes one byte per bit (values 0/1, data.rs:36) — a CUDA uint8 tensor
+    (asynchronous, on the current stream) or a numpy array — and returns the samples of
+    every complete symbol: (n, 2) interleaved (i, q) for the IQ modes, (n,) for OUT_REAL.
+    `taps=None` keeps the reference's sample-and-hold (bit-compatible with `modulate --iq`).
+    `carrier.sample` advances by the samples produced, as the shared `&mut Carrier` does.
+    """
+
+    def __init__(self, carrier: Carrier, phasor: _Phasor, samples_per_symbol: int,
+                 taps: Optional[np.ndarray] = None, dtype: int = DTYPE_F32,
+                 out_mode: int = OUT_IQ_MIXED, device: int = 0):
+        L = load_library()
+        self.carrier, self.phasor = carrier, phasor
+        self.sps, self.dtype, self.out_mode, self.device = int(samples_per_symbol), dtype, out_mode, device
+        self.bps = phasor.bits_per_symbol()
+        self._lut = phasor.lut()
+        self.taps = None if taps is None else np.ascontiguousarray(taps, dtype=np.float32)
+        d = _TxDesc()
+        d.bits_per_symbol = self.bps
+        d.lut = _fptr(self._lut)
+        d.samples_per_symbol = self.sps
+        d.taps = _fptr(self.taps) if self.taps is not None else None
+        d.ntaps = 0 if self.taps is None else len(self.taps)
+        d.sample_freq = carrier.sample_freq
+        d.s0 = carrier.sample
+        d.dtype, d.out_mode = dtype, out_mode
+        h = ctypes.c_void_p()
+        _check(L.modem_tx_create(ctypes.byref(d), device, ctypes.byref(h)), "DigitalModulator")
+        self._h = h
+        self._ncarry = 0
+
+    def _alloc(self, ref, nsamp: int):
+        npd = np.float16 if self.dtype == DTYPE_F16 else np.float32
+        shape = (nsamp,) if self.out_mode == OUT_REAL else (nsamp, 2)
+        return _empty_like_input(ref, shape, npd)
+
+    def nsamples(self, nbits: int) -> int:
+        return ((self._ncarry + nbits) // self.bps) * self.sps
+
+    def process(self, bits, out=None, stream=None):
+        n = int(bits.numel() if _is_torch(bits) else bits.size)
+        ns = self.nsamples(n)
+        if out is None:
+            out = self._alloc(bits, ns)
+        cap = int(out.shape[0])
+        prod = ctypes.c_size_t()
+        _check(load_library().modem_tx_process(self._h, _ptr(bits), n, _ptr(out), cap,
+                                               ctypes.byref(prod), _stream_handle(stream)),
+               "DigitalModulator.process")
+        self._ncarry = (self._ncarry + n) % self.bps
+        self.carrier.sample = int(load_library().modem_tx_sample(self._h))
+        return out[: prod.value]
+
+    def flush(self, like=None, stream=None):
+        ntaps = 0 if self.taps is None else len(self.taps)
+        ns = ((max(ntaps - 1, 0) + self.sps - 1) // self.sps) * self.sps
+        ref = like if like is not None else np.zeros(1, np.uint8)
+        out = self._alloc(ref, ns)
+        prod = ctypes.c_size_t()
+        _check(load_library().modem_tx_flush(self._h, _ptr(out), int(out.shape[0]), ctypes.byref(prod),
+                                             _stream_handle(stream)), "DigitalModulator.flush")
+        self.carrier.sample = int(load_library().modem_tx_sample(self._h))
+        return out[: prod.value]
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.modem_tx_destroy(self._h)
+            self._h = None
+
+
+# ------------------------------------------------------------------- RX (B6+B5) ----
+class DemodulatorRx:
+    """Demodulator (demodulator.rs:7-56) + matched filter + decimation + slicer.
+
+    mix=MIX_REFERENCE_REAL, decim=1 is the reference Demodulator exactly (real input
+    x.re, (2*FIR(x cos), 2*FIR(-x sin)) at every sample, PLL offset 0). The loopback
+    contract uses MIX_COMPLEX with decim = samples/symbol and decim_offset = ntaps-1.
+    """
+
+    def __init__(self, carrier: Carrier, taps: np.ndarray, decim: int = 1, decim_offset: int = 0,
+                 mix: int = MIX_REFERENCE_REAL, slicer: Optional[_SlicerDesc] = None,
+                 in_dtype: int = DTYPE_F32, out_dtype: int = DTYPE_F32, device: int = 0):
+        L = load_library()
+        self.carrier, self.decim, self.out_dtype, self.in_dtype = carrier, int(decim), out_dtype, in_dtype
+        self.taps = np.ascontiguousarray(taps, dtype=np.float32)
+        self.decim_offset = int(decim_offset)
+        d = _RxDesc()
+        d.sample_freq = carrier.sample_freq
+        d.s0 = carrier.sample
+        d.taps = _fptr(self.taps)
+        d.ntaps = len(self.taps)
+        d.decim, d.decim_offset, d.mix = self.decim, self.decim_offset, mix
+        d.in_dtype, d.out_dtype = in_dtype, out_dtype
+        if slicer is not None:
+            d.slicer = slicer
+        else:
+            d.slicer.kind = SLICER_NONE
+        self._slicer = slicer
+        h = ctypes.c_void_p()
+        _check(L.modem_rx_create(ctypes.byref(d), device, ctypes.byref(h)), "Demodulator")
+        self._h = h
+        self._consumed = 0
+
+    def noutputs(self, n: int) -> int:
+        def first(x):
+            return 0 if x <= self.decim_offset else (x - self.decim_offset + self.decim - 1) // self.decim
+        a, b = first(self._consumed), first(self._consumed + n)
+        return max(0, b - a)
+
+    def process(self, iq, want_iq: bool = True, want_sym: bool = True, stream=None):
+        n = int(iq.shape[0])
+        nout = self.noutputs(n)
+        npd = np.float16 if self.out_dtype == DTYPE_F16 else np.float32
+        oiq = _empty_like_input(iq, (nout, 2), npd) if want_iq else None
+        osym = _empty_like_input(iq, (nout,), np.uint8) if (want_sym and self._slicer is not None) else None
+        prod = ctypes.c_size_t()
+        _check(load_library().modem_rx_process(self._h, _ptr(iq), n, _ptr(oiq), _ptr(osym), nout,
+                                               ctypes.byref(prod), _stream_handle(stream)),
+               "Demodulator.process")
+        self._consumed += n
+        self.carrier.sample = int(load_library().modem_rx_sample(self._h))
+        return (None if oiq is None else oiq[: prod.value]), (None if osym is None else osym[: prod.value])
+
+    def flush(self, like=None, stream=None):
+        n = len(self.taps) - 1
+        nout = self.noutputs(n)
+        ref = like if like is not None else np.zeros(1, np.float32)
+        npd = np.float16 if self.out_dtype == DTYPE_F16 else np.float32
+        oiq = _empty_like_input(ref, (nout, 2), npd)
+        osym = _empty_like_input(ref, (nout,), np.uint8) if self._slicer is not None else None
+        prod = ctypes.c_size_t()
+        _check(load_library().modem_rx_flush(self._h, _ptr(oiq), _ptr(osym), nout, ctypes.byref(prod),
+                                             _stream_handle(stream)), "Demodulator.flush")
+        self._consumed += n
+        self.carrier.sample = int(load_library().modem_rx_sample(self._h))
+        return oiq[: prod.value], (None if osym is None else osym[: prod.value])
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.modem_rx_destroy(self._h)
+            self._h = None
+
+
+# --------------------------------------------------------------------- FIR (B5) ----
+class FIRFilter:
+    """FIRFilter (fir.rs:3-35): causal FIR, zero initial history, one output per input."""
+
+    def __init__(self, coefs, device: int = 0):
+        self.coefs = np.ascontiguousarray(coefs, dtype=np.float32)
+        if len(self.coefs) == 0:
+            raise ModemPanic(ERR_INVALID_ARG, "FIRFilter: attempt to calculate the remainder with a divisor of zero")
+        h = ctypes.c_void_p()
+        _check(load_library().modem_fir_create(_fptr(self.coefs), len(self.coefs), device, ctypes.byref(h)),
+               "FIRFilter")
+        self._h = h
+
+    def process(self, x, stream=None):
+        n = int(x.shape[0])
+        y = _empty_like_input(x, (n,), np.float32)
+        _check(load_library().modem_fir_process(self._h, _ptr(x), _ptr(y), n, _stream_handle(stream)),
+               "FIRFilter.process")
+        return y
+
+    def add(self, sample: float) -> float:
+        return float(self.process(np.array([sample], dtype=np.float32))[0])
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.modem_fir_destroy(self._h)
+            self._h = None
+
+
+def prng_bits(seed: int, nbits: int, device: int = 0, stream=None):
+    """Synthetic bit stream (GLUE): splitmix64, one byte per bit, on the device."""
+    import torch
+    out = torch.empty(int(nbits), dtype=torch.uint8, device=f"cuda:{device}")
+    _check(load_library().modem_prng_bits(int(seed), out.data_ptr() if nbits else None, int(nbits), device,
+                                          _stream_handle(stream)), "prng_bits")
+    return out

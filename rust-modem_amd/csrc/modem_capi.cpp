@@ -1,0 +1,674 @@
+// rust-modem_amd/csrc/modem_capi.cpp — implementation of include/modem_hip.h.
+//
+// Host side of the drop-in boundary: phasor LUT builders (the memoryless DigitalPhasor
+// plugins evaluated once per symbol value, same expressions and rounding as the reference),
+// RRC tap generation, and the streaming TX / RX / FIR handles that own device state and
+// launch the kernels of modem_kernels.hip. Built with -ffp-contract=off so host float
+// expressions round like rustc's.
+#include "../../include/modem_hip.h"
+#include "modem_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float kPi = 3.14159265358979323846f;   // std::f32::consts::PI
+
+struct DeviceGuard {   // scoped hipSetDevice
+    int old = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&old) != hipSuccess) { (void)hipGetLastError(); old = -1; }
+        ok = hipSetDevice(dev) == hipSuccess;
+        if (!ok) (void)hipGetLastError();
+    }
+    ~DeviceGuard() { if (old >= 0) (void)hipSetDevice(old); }
+};
+
+bool is_device_ptr(const void* p) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+#define HIP_TRY(expr)                                                              \
+    do {                                                                           \
+        if ((expr) != hipSuccess) { (void)hipGetLastError(); return MODEM_ERR_HIP; } \
+    } while (0)
+
+template <typename T>
+modem_status dalloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    if (hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)) != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return MODEM_ERR_ALLOC;
+    }
+    if (hipMemset(*p, 0, count * sizeof(T)) != hipSuccess) { (void)hipGetLastError(); return MODEM_ERR_HIP; }
+    return MODEM_OK;
+}
+
+// Growable device staging buffer for host-pointer I/O.
+struct Stage {
+    void* p = nullptr;
+    size_t cap = 0;
+    modem_status ensure(size_t bytes) {
+        if (bytes <= cap) return MODEM_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr; cap = 0;
+        if (hipMalloc(&p, bytes) != hipSuccess) { (void)hipGetLastError(); p = nullptr; return MODEM_ERR_ALLOC; }
+        cap = bytes;
+        return MODEM_OK;
+    }
+    ~Stage() { if (p) (void)hipFree(p); }
+};
+
+bool device_ok(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return device >= 0 && device < n;
+}
+
+// ---- reference restatements used by the LUT builder (digital/util.rs, util.rs) ----------
+float bit_to_sign(uint8_t b) { return (float)(int8_t)(2 * (int8_t)b - 1); }   // digital/util.rs:1-3
+uint8_t bytes_to_bits(const uint8_t* b, size_t n) {                            // digital/util.rs:5-11
+    if (n == 0) return 0;
+    uint8_t s = 0;
+    for (size_t i = 0; i < n; ++i) s = (uint8_t)(s | (uint8_t)((b[i] & 1) << (n - 1 - i)));
+    return s;
+}
+float mod_trig(float x) {                                                      // util.rs:3-6
+    const float two_pi = kPi * 2.0f;
+    return x - two_pi * std::floor(x / two_pi);
+}
+
+modem_status phasor_bps(const modem_phasor_desc* d, uint32_t* bps) {
+    switch (d->kind) {
+    case MODEM_PHASOR_BPSK: case MODEM_PHASOR_BASK: *bps = 1; return MODEM_OK;
+    case MODEM_PHASOR_QPSK: case MODEM_PHASOR_OQPSK: *bps = 2; return MODEM_OK;
+    case MODEM_PHASOR_QAM:
+        if (d->bits_per_symbol < 2 || d->bits_per_symbol > 8) return MODEM_ERR_INVALID_ARG;  // qam.rs:17
+        *bps = d->bits_per_symbol; return MODEM_OK;
+    case MODEM_PHASOR_MPSK: case MODEM_PHASOR_APSK:
+        if (d->bits_per_symbol < 1 || d->bits_per_symbol > 8) return MODEM_ERR_INVALID_ARG;
+        *bps = d->bits_per_symbol; return MODEM_OK;
+    default: return MODEM_ERR_INVALID_ARG;
+    }
+}
+
+// i(_, b), q(_, b) of one memoryless phasor for the bit slice b (MSB first).
+modem_status phasor_iq(const modem_phasor_desc* d, const uint8_t* b, size_t n, float* i, float* q) {
+    const float A = d->amplitude;
+    switch (d->kind) {
+    case MODEM_PHASOR_BPSK: {                                     // bpsk.rs:17-31
+        const float c = bit_to_sign(b[0]) * A;
+        *i = c * std::cos(d->phase); *q = c * std::sin(d->phase);
+        return MODEM_OK;
+    }
+    case MODEM_PHASOR_QPSK: {                                     // qpsk.rs:11-35
+        const float pc = std::cos(d->phase), ps = std::sin(d->phase);
+        const float amp = A * std::sqrt(0.5f);
+        *i = amp * (bit_to_sign(b[0]) * pc - bit_to_sign(b[1]) * ps);
+        *q = amp * (bit_to_sign(b[1]) * pc + bit_to_sign(b[0]) * ps);
+        return MODEM_OK;
+    }
+    case MODEM_PHASOR_QAM: {                                      // qam.rs:15-60
+        const size_t cs = n / 2;
+        const float ms = (float)((1u << cs) - 1);
+        const float pc = std::cos(d->phase), ps = std::sin(d->phase);
+        const float amp = A / ms / 2.0f;
+        const float pm = 2.0f * (float)bytes_to_bits(b, cs) - ms;
+        const float pl = 2.0f * (float)bytes_to_bits(b + cs, n - cs) - ms;
+        *i = amp * (pm * pc - pl * ps);
+        *q = amp * (pl * pc + pm * ps);
+        return MODEM_OK;
+    }
+    case MODEM_PHASOR_BASK:                                       // bask.rs:15-24
+        *i = (float)b[0] * A; *q = 0.0f;
+        return MODEM_OK;
+    case MODEM_PHASOR_MPSK: {                                     // mpsk.rs:14-41
+        const float ns = (float)(1u << n);
+        const float inner = 2.0f * kPi * (float)bytes_to_bits(b, n) / ns + d->phase;
+        *i = A * std::cos(inner); *q = A * std::sin(inner);
+        return MODEM_OK;
+    }
+    case MODEM_PHASOR_APSK: {                                     // apsk.rs:36-56
+        const uint8_t s = bytes_to_bits(b, n);
+        const modem_ring* ring = nullptr;
+        for (uint32_t k = 0; k < d->nrings; ++k)
+            if (s >= d->rings[k].start && s < d->rings[k].end) { ring = &d->rings[k]; break; }
+        if (!ring) return MODEM_ERR_INVALID_ARG;
+        const float inner = 2.0f * kPi * (float)(uint8_t)(s - ring->start) /
+                            (float)(uint8_t)(ring->end - ring->start) + ring->phase;
+        *i = A * ring->radius * std::cos(inner); *q = A * ring->radius * std::sin(inner);
+        return MODEM_OK;
+    }
+    case MODEM_PHASOR_OQPSK: {                                    // oqpsk.rs:9-25
+        const float amp = A * std::sqrt(0.5f);
+        *i = bit_to_sign(b[0]) * amp; *q = bit_to_sign(b[1]) * amp;
+        return MODEM_OK;
+    }
+    default: return MODEM_ERR_INVALID_ARG;
+    }
+}
+
+modem_status apsk_verify(const modem_phasor_desc* d, uint32_t bps) {   // apsk.rs:25-26,74,85-97
+    if (d->nrings == 0 || !d->rings) return MODEM_ERR_INVALID_ARG;
+    unsigned prev = 0;
+    for (uint32_t k = 0; k < d->nrings; ++k) {
+        const modem_ring& r = d->rings[k];
+        if (!(r.radius >= 0.0f && r.radius <= 1.0f)) return MODEM_ERR_INVALID_ARG;
+        if (r.start != prev) return MODEM_ERR_INVALID_ARG;
+        prev = r.end;
+    }
+    return prev == (1u << bps) ? MODEM_OK : MODEM_ERR_INVALID_ARG;
+}
+
+}  // namespace
+
+// =====================================================================================
+extern "C" {
+
+const char* modem_status_str(modem_status s) {
+    switch (s) {
+    case MODEM_OK: return "ok";
+    case MODEM_ERR_INVALID_ARG: return "invalid argument (the reference would panic)";
+    case MODEM_ERR_UNSUPPORTED: return "unsupported by this backend";
+    case MODEM_ERR_HIP: return "HIP runtime error";
+    case MODEM_ERR_NO_DEVICE: return "no such HIP device";
+    case MODEM_ERR_CAPACITY: return "output buffer too small";
+    case MODEM_ERR_ALLOC: return "allocation failed";
+    }
+    return "unknown status";
+}
+
+int32_t modem_abi_version(void) { return MODEM_HIP_ABI_VERSION; }
+
+float modem_freq_sample_freq(uint64_t hz, uint64_t sr) {           // freq.rs:19-26
+    const float ang = 2.0f * kPi * (float)hz;
+    return ang / (float)sr;
+}
+
+modem_status modem_rates_sps(uint64_t br, uint64_t sr, uint64_t* sps) {   // rates.rs:12-18
+    if (!sps || br == 0) return MODEM_ERR_INVALID_ARG;
+    *sps = sr / br;
+    return MODEM_OK;
+}
+
+float modem_carrier_phase(float w, uint64_t n) { return mod_trig(w * (float)n); }   // carrier.rs:17-19
+
+modem_status modem_carrier_phases(float w, uint64_t s0, size_t n, float* out, int device, void* stream) {
+    if (n && (!out || !is_device_ptr(out))) return MODEM_ERR_INVALID_ARG;
+    if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    HIP_TRY(mk::launch_phases(w, s0, n, out, (hipStream_t)stream));
+    return MODEM_OK;
+}
+
+modem_status modem_phasor_bits(const modem_phasor_desc* d, uint32_t* bps) {
+    if (!d || !bps) return MODEM_ERR_INVALID_ARG;
+    return phasor_bps(d, bps);
+}
+
+modem_status modem_phasor_lut(const modem_phasor_desc* d, float* lut) {
+    if (!d || !lut) return MODEM_ERR_INVALID_ARG;
+    uint32_t bps;
+    modem_status st = phasor_bps(d, &bps);
+    if (st) return st;
+    if (d->kind == MODEM_PHASOR_APSK && (st = apsk_verify(d, bps))) return st;
+    uint8_t b[8];
+    for (uint32_t s = 0; s < (1u << bps); ++s) {
+        for (uint32_t k = 0; k < bps; ++k) b[k] = (uint8_t)((s >> (bps - 1 - k)) & 1u);
+        if ((st = phasor_iq(d, b, bps, &lut[2 * s], &lut[2 * s + 1]))) return st;
+    }
+    return MODEM_OK;
+}
+
+modem_status modem_phasor_slicer(const modem_phasor_desc* d, const float* lut, modem_slicer_desc* o) {
+    if (!d || !o) return MODEM_ERR_INVALID_ARG;
+    uint32_t bps;
+    modem_status st = phasor_bps(d, &bps);
+    if (st) return st;
+    std::memset(o, 0, sizeof *o);
+    o->bits_per_symbol = bps;
+    if (d->kind == MODEM_PHASOR_QAM && d->phase == 0.0f && bps % 2 == 0 && d->amplitude > 0.0f) {
+        const uint32_t cs = bps / 2;
+        const float ms = (float)((1u << cs) - 1);
+        o->kind = MODEM_SLICER_QAM_AXIS;
+        o->bits_per_carrier = cs;
+        o->max_symbol = ms;
+        o->inv_scale = 1.0f / (d->amplitude / ms / 2.0f);     // qam.rs:28
+        return MODEM_OK;
+    }
+    if (!lut) return MODEM_ERR_INVALID_ARG;
+    o->kind = MODEM_SLICER_NEAREST;
+    o->lut = lut;
+    return MODEM_OK;
+}
+
+modem_status modem_rrc_taps(uint32_t L, uint32_t sps, double beta, float* out) {
+    if (!out || L == 0 || sps == 0 || !(beta >= 0.0 && beta <= 1.0)) return MODEM_ERR_INVALID_ARG;
+    const double pi = 3.14159265358979323846;
+    std::vector<double> h(L);
+    double e = 0.0;
+    for (uint32_t i = 0; i < L; ++i) {
+        const double t = ((double)i - (double)(L - 1) / 2.0) / (double)sps;
+        double v;
+        if (t == 0.0) v = 1.0 - beta + 4.0 * beta / pi;
+        else if (beta > 0.0 && std::fabs(std::fabs(4.0 * beta * t) - 1.0) < 1e-12)
+            v = beta / std::sqrt(2.0) * ((1.0 + 2.0 / pi) * std::sin(pi / (4.0 * beta)) +
+                                         (1.0 - 2.0 / pi) * std::cos(pi / (4.0 * beta)));
+        else
+            v = (std::sin(pi * t * (1.0 - beta)) + 4.0 * beta * t * std::cos(pi * t * (1.0 + beta))) /
+                (pi * t * (1.0 - (4.0 * beta * t) * (4.0 * beta * t)));
+        h[i] = v;
+        e += v * v;
+    }
+    const double g = 1.0 / std::sqrt(e);
+    for (uint32_t i = 0; i < L; ++i) out[i] = (float)(h[i] * g);
+    return MODEM_OK;
+}
+
+// ------------------------------------------------------------------------------ TX ----
+struct modem_tx {
+    int device = 0;
+    uint32_t bps = 0, sps = 0, ntaps = 0, K = 1;
+    float w = 0.f;
+    uint64_t sample = 0;
+    int dtype = 0, out_mode = 0;
+    float2* d_lut = nullptr;
+    float* d_taps = nullptr;
+    float2* d_hist[2] = {nullptr, nullptr};
+    uint8_t* d_carry[2] = {nullptr, nullptr};
+    int hcur = 0, ccur = 0, ncarry = 0;
+    Stage bits_stage, out_stage;
+    ~modem_tx() {
+        DeviceGuard g(device);
+        for (void* p : {(void*)d_lut, (void*)d_taps, (void*)d_hist[0], (void*)d_hist[1],
+                        (void*)d_carry[0], (void*)d_carry[1]})
+            if (p) (void)hipFree(p);
+    }
+};
+
+static size_t tx_sample_bytes(const modem_tx* h) {
+    const size_t v = h->dtype == MODEM_DTYPE_F16 ? 2 : 4;
+    return h->out_mode == MODEM_OUT_REAL ? v : 2 * v;
+}
+
+modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out) {
+    if (!d || !out) return MODEM_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (d->bits_per_symbol < 1 || d->bits_per_symbol > 8 || !d->lut) return MODEM_ERR_INVALID_ARG;
+    if (d->samples_per_symbol < 1) return MODEM_ERR_INVALID_ARG;   // SymbolClock % 0 panics (data.rs:29)
+    if (d->ntaps > (uint32_t)mk::kMaxTaps || (d->ntaps && !d->taps)) return MODEM_ERR_INVALID_ARG;
+    if (d->dtype != MODEM_DTYPE_F32 && d->dtype != MODEM_DTYPE_F16) return MODEM_ERR_INVALID_ARG;
+    if (d->out_mode < MODEM_OUT_IQ_MIXED || d->out_mode > MODEM_OUT_REAL) return MODEM_ERR_INVALID_ARG;
+    if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_tx* h = new (std::nothrow) modem_tx;
+    if (!h) return MODEM_ERR_ALLOC;
+    h->device = device;
+    h->bps = d->bits_per_symbol;
+    h->sps = d->samples_per_symbol;
+    h->ntaps = d->ntaps;
+    h->w = d->sample_freq;
+    h->sample = d->s0;
+    h->dtype = d->dtype;
+    h->out_mode = d->out_mode;
+    // ntaps == 0: the reference's sample-and-hold == zero-stuffing + sps unit taps.
+    const uint32_t L = d->ntaps ? d->ntaps : d->samples_per_symbol;
+    h->K = (L + h->sps - 1) / h->sps;
+    std::vector<float> pp((size_t)h->K * h->sps, 0.0f);   // pp[t*sps + p] = h[p + sps*t]
+    for (uint32_t j = 0; j < L; ++j) pp[(size_t)(j / h->sps) * h->sps + j % h->sps] = d->ntaps ? d->taps[j] : 1.0f;
+    modem_status st;
+    const size_t nl = (size_t)1 << h->bps;
+    if ((st = dalloc(&h->d_lut, nl)) || (st = dalloc(&h->d_taps, pp.size())) ||
+        (st = dalloc(&h->d_hist[0], h->K)) || (st = dalloc(&h->d_hist[1], h->K)) ||
+        (st = dalloc(&h->d_carry[0], 8)) || (st = dalloc(&h->d_carry[1], 8))) {
+        delete h;
+        return st;
+    }
+    if (hipMemcpy(h->d_lut, d->lut, nl * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->d_taps, pp.data(), pp.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipGetLastError();
+        delete h;
+        return MODEM_ERR_HIP;
+    }
+    *out = h;
+    return MODEM_OK;
+}
+
+static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool flush, void* out,
+                           size_t cap, size_t* produced, hipStream_t s) {
+    if (!h || !produced || (nbits && !bits)) return MODEM_ERR_INVALID_ARG;
+    *produced = 0;
+    const uint64_t total = (uint64_t)h->ncarry + nbits;
+    const int64_t nsym = flush ? (int64_t)((h->ntaps ? h->ntaps - 1 : 0) + h->sps - 1) / h->sps
+                               : (int64_t)(total / h->bps);
+    const int ncarry_new = flush ? h->ncarry : (int)(total - (uint64_t)nsym * h->bps);
+    const size_t nsamp = (size_t)nsym * h->sps;
+    if (nsamp > cap) return MODEM_ERR_CAPACITY;
+    if (nsamp && !out) return MODEM_ERR_INVALID_ARG;
+    DeviceGuard g(h->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_status st;
+    const uint8_t* dbits = bits;
+    if (nbits && !is_device_ptr(bits)) {
+        if ((st = h->bits_stage.ensure(nbits))) return st;
+        HIP_TRY(hipMemcpyAsync(h->bits_stage.p, bits, nbits, hipMemcpyHostToDevice, s));
+        dbits = static_cast<const uint8_t*>(h->bits_stage.p);
+    }
+    const bool host_out = nsamp && !is_device_ptr(out);
+    void* dout = out;
+    if (host_out) {
+        if ((st = h->out_stage.ensure(nsamp * tx_sample_bytes(h)))) return st;
+        dout = h->out_stage.p;
+    }
+    mk::TxParams p{};
+    p.bits = dbits;
+    p.carry = h->d_carry[h->ccur];
+    p.carry_new = h->d_carry[h->ccur ^ 1];
+    p.hist = h->d_hist[h->hcur];
+    p.hist_new = h->d_hist[h->hcur ^ 1];
+    p.lut = h->d_lut;
+    p.taps = h->d_taps;
+    p.out = dout;
+    p.s0 = h->sample;
+    p.nsym = nsym;
+    p.nsym_valid = flush ? 0 : nsym;
+    p.nbits = (int64_t)nbits;
+    p.ncarry = h->ncarry;
+    p.ncarry_new = ncarry_new;
+    p.update_carry = flush ? 0 : 1;
+    p.bps = (int)h->bps;
+    p.sps = (int)h->sps;
+    p.K = (int)h->K;
+    p.fast_bits = (h->ncarry == 0 && (h->bps == 1 || h->bps == 2 || h->bps == 4 || h->bps == 8) &&
+                   ((uintptr_t)dbits % h->bps) == 0) ? 1 : 0;
+    p.small_n = (h->sample + nsamp) <= (1ull << 32) ? 1 : 0;
+    p.w = h->w;
+    HIP_TRY(mk::launch_tx(p, (int)h->sps, h->dtype, h->out_mode, s));
+    h->hcur ^= 1;
+    if (!flush) { h->ccur ^= 1; h->ncarry = ncarry_new; }
+    h->sample += nsamp;
+    if (host_out) {
+        HIP_TRY(hipMemcpyAsync(out, dout, nsamp * tx_sample_bytes(h), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    } else if (nbits && dbits != bits) {
+        HIP_TRY(hipStreamSynchronize(s));   // host bits staged: keep the caller's view simple
+    }
+    *produced = nsamp;
+    return MODEM_OK;
+}
+
+modem_status modem_tx_process(modem_tx* h, const uint8_t* bits, size_t nbits, void* out, size_t cap,
+                              size_t* produced, void* stream) {
+    return tx_run(h, bits, nbits, false, out, cap, produced, (hipStream_t)stream);
+}
+modem_status modem_tx_flush(modem_tx* h, void* out, size_t cap, size_t* produced, void* stream) {
+    return tx_run(h, nullptr, 0, true, out, cap, produced, (hipStream_t)stream);
+}
+uint64_t modem_tx_sample(const modem_tx* h) { return h ? h->sample : 0; }
+modem_status modem_tx_destroy(modem_tx* h) { delete h; return MODEM_OK; }
+
+// ------------------------------------------------------------------------------ RX ----
+struct modem_rx {
+    int device = 0;
+    uint32_t ntaps = 0, decim = 1, D = 0, K = 1, HL = 0;
+    int mix = 0, in_dtype = 0, out_dtype = 0;
+    float w = 0.f;
+    uint64_t c0 = 0;
+    int64_t consumed = 0;          // stream samples processed
+    modem_slicer_desc slicer{};
+    float* d_taps = nullptr;
+    float2* d_slut = nullptr;
+    void* d_hist[2] = {nullptr, nullptr};
+    void* d_zeros = nullptr;
+    int hcur = 0;
+    Stage in_stage, iq_stage, sym_stage;
+    ~modem_rx() {
+        DeviceGuard g(device);
+        for (void* p : {(void*)d_taps, (void*)d_slut, d_hist[0], d_hist[1], d_zeros})
+            if (p) (void)hipFree(p);
+    }
+};
+
+static size_t rx_in_bytes(const modem_rx* h) { return h->in_dtype == MODEM_DTYPE_F16 ? 4 : 8; }
+static size_t rx_out_bytes(const modem_rx* h) { return h->out_dtype == MODEM_DTYPE_F16 ? 4 : 8; }
+
+modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out) {
+    if (!d || !out) return MODEM_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (d->ntaps < 1 || d->ntaps > (uint32_t)mk::kMaxTaps || !d->taps) return MODEM_ERR_INVALID_ARG;
+    if (d->decim < 1) return MODEM_ERR_INVALID_ARG;
+    if (d->mix != MODEM_MIX_COMPLEX && d->mix != MODEM_MIX_REFERENCE_REAL) return MODEM_ERR_INVALID_ARG;
+    if ((d->in_dtype != MODEM_DTYPE_F32 && d->in_dtype != MODEM_DTYPE_F16) ||
+        (d->out_dtype != MODEM_DTYPE_F32 && d->out_dtype != MODEM_DTYPE_F16)) return MODEM_ERR_INVALID_ARG;
+    const modem_slicer_desc& sl = d->slicer;
+    if (sl.kind == MODEM_SLICER_NEAREST && (sl.bits_per_symbol < 1 || sl.bits_per_symbol > 8 || !sl.lut))
+        return MODEM_ERR_INVALID_ARG;
+    if (sl.kind == MODEM_SLICER_QAM_AXIS && (sl.bits_per_carrier < 1 || sl.bits_per_carrier > 4))
+        return MODEM_ERR_INVALID_ARG;
+    if (sl.kind < MODEM_SLICER_NONE || sl.kind > MODEM_SLICER_QAM_AXIS) return MODEM_ERR_INVALID_ARG;
+    if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_rx* h = new (std::nothrow) modem_rx;
+    if (!h) return MODEM_ERR_ALLOC;
+    h->device = device;
+    h->ntaps = d->ntaps;
+    h->decim = d->decim;
+    h->D = d->decim_offset;
+    h->K = (d->ntaps + d->decim - 1) / d->decim;
+    h->HL = h->K * h->decim - 1;
+    h->mix = d->mix;
+    h->in_dtype = d->in_dtype;
+    h->out_dtype = d->out_dtype;
+    h->w = d->sample_freq;
+    h->c0 = d->s0;
+    h->slicer = sl;
+    h->slicer.lut = nullptr;
+    std::vector<float> pp((size_t)h->K * h->decim, 0.0f);   // pp[b*K + t] = h[b + decim*t]
+    for (uint32_t j = 0; j < d->ntaps; ++j) pp[(size_t)(j % h->decim) * h->K + j / h->decim] = d->taps[j];
+    const size_t esz = rx_in_bytes(h);
+    modem_status st;
+    uint8_t *h0 = nullptr, *h1 = nullptr, *z = nullptr;
+    if ((st = dalloc(&h->d_taps, pp.size())) || (st = dalloc(&h->d_slut, 256)) ||
+        (st = dalloc(&h0, (h->HL + 1) * esz)) || (st = dalloc(&h1, (h->HL + 1) * esz)) ||
+        (st = dalloc(&z, (size_t)(h->ntaps) * esz))) {
+        h->d_hist[0] = h0; h->d_hist[1] = h1; h->d_zeros = z;
+        delete h;
+        return st;
+    }
+    h->d_hist[0] = h0; h->d_hist[1] = h1; h->d_zeros = z;
+    if (hipMemcpy(h->d_taps, pp.data(), pp.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
+    }
+    if (sl.kind == MODEM_SLICER_NEAREST &&
+        hipMemcpy(h->d_slut, sl.lut, ((size_t)2 << sl.bits_per_symbol) * sizeof(float),
+                  hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
+    }
+    *out = h;
+    return MODEM_OK;
+}
+
+// Kept instants n = k*decim + D with n in [a, b): first k and count.
+static void rx_range(int64_t a, int64_t b, int64_t decim, int64_t D, int64_t* k0, int64_t* cnt) {
+    auto first_at_or_after = [&](int64_t n) -> int64_t {
+        return n <= D ? 0 : (n - D + decim - 1) / decim;
+    };
+    *k0 = first_at_or_after(a);
+    const int64_t k1 = first_at_or_after(b);
+    *cnt = k1 > *k0 ? k1 - *k0 : 0;
+}
+
+static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, void* out_iq,
+                           uint8_t* out_sym, size_t cap, size_t* produced, hipStream_t s) {
+    if (!h || !produced || (n && !in && !zeros)) return MODEM_ERR_INVALID_ARG;
+    *produced = 0;
+    int64_t k_first, nout;
+    rx_range(h->consumed, h->consumed + (int64_t)n, h->decim, h->D, &k_first, &nout);
+    if ((size_t)nout > cap) return MODEM_ERR_CAPACITY;
+    DeviceGuard g(h->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_status st;
+    const void* din = zeros ? h->d_zeros : in;
+    if (n && !zeros && !is_device_ptr(in)) {
+        if ((st = h->in_stage.ensure(n * rx_in_bytes(h)))) return st;
+        HIP_TRY(hipMemcpyAsync(h->in_stage.p, in, n * rx_in_bytes(h), hipMemcpyHostToDevice, s));
+        din = h->in_stage.p;
+    }
+    const bool host_iq = nout && out_iq && !is_device_ptr(out_iq);
+    const bool host_sym = nout && out_sym && !is_device_ptr(out_sym);
+    void* diq = out_iq;
+    uint8_t* dsym = out_sym;
+    if (host_iq) {
+        if ((st = h->iq_stage.ensure((size_t)nout * rx_out_bytes(h)))) return st;
+        diq = h->iq_stage.p;
+    }
+    if (host_sym) {
+        if ((st = h->sym_stage.ensure((size_t)nout))) return st;
+        dsym = static_cast<uint8_t*>(h->sym_stage.p);
+    }
+    mk::RxParams p{};
+    p.x = din;
+    p.hist = h->d_hist[h->hcur];
+    p.hist_new = h->d_hist[h->hcur ^ 1];
+    p.out_iq = nout ? diq : nullptr;
+    p.out_sym = nout ? dsym : nullptr;
+    p.taps = h->d_taps;
+    p.slut = h->d_slut;
+    p.N = (int64_t)n;
+    p.n_start = h->consumed;
+    p.c0 = h->c0;
+    p.k_first = k_first;
+    p.nout = nout;
+    p.K = (int)h->K;
+    p.L = (int)h->ntaps;
+    p.HL = (int)h->HL;
+    p.D = (int)h->D;
+    p.decim = (int)h->decim;
+    p.x_aligned16 = ((uintptr_t)din % 16) == 0 ? 1 : 0;
+    p.small_n = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 32) ? 1 : 0;
+    p.slicer_kind = h->slicer.kind;
+    p.bps = (int)h->slicer.bits_per_symbol;
+    p.bits_per_carrier = (int)h->slicer.bits_per_carrier;
+    p.inv_scale = h->slicer.inv_scale;
+    p.max_symbol = h->slicer.max_symbol;
+    p.w = h->w;
+    HIP_TRY(mk::launch_rx(p, (int)h->decim, h->in_dtype, h->out_dtype, h->mix, s));
+    h->hcur ^= 1;
+    h->consumed += (int64_t)n;
+    if (host_iq) HIP_TRY(hipMemcpyAsync(out_iq, diq, (size_t)nout * rx_out_bytes(h), hipMemcpyDeviceToHost, s));
+    if (host_sym) HIP_TRY(hipMemcpyAsync(out_sym, dsym, (size_t)nout, hipMemcpyDeviceToHost, s));
+    if (host_iq || host_sym || din == h->in_stage.p) HIP_TRY(hipStreamSynchronize(s));
+    *produced = (size_t)nout;
+    return MODEM_OK;
+}
+
+modem_status modem_rx_process(modem_rx* h, const void* in, size_t n, void* out_iq, uint8_t* out_sym,
+                              size_t cap, size_t* produced, void* stream) {
+    return rx_run(h, in, n, false, out_iq, out_sym, cap, produced, (hipStream_t)stream);
+}
+modem_status modem_rx_flush(modem_rx* h, void* out_iq, uint8_t* out_sym, size_t cap, size_t* produced,
+                            void* stream) {
+    if (!h) return MODEM_ERR_INVALID_ARG;
+    return rx_run(h, nullptr, h->ntaps - 1, true, out_iq, out_sym, cap, produced, (hipStream_t)stream);
+}
+uint64_t modem_rx_sample(const modem_rx* h) { return h ? h->c0 + (uint64_t)h->consumed : 0; }
+modem_status modem_rx_destroy(modem_rx* h) { delete h; return MODEM_OK; }
+
+// ----------------------------------------------------------------------------- FIR ----
+struct modem_fir {
+    int device = 0;
+    uint32_t L = 0;
+    float* d_taps = nullptr;
+    float* d_hist[2] = {nullptr, nullptr};
+    int hcur = 0;
+    Stage in_stage, out_stage;
+    ~modem_fir() {
+        DeviceGuard g(device);
+        for (void* p : {(void*)d_taps, (void*)d_hist[0], (void*)d_hist[1]}) if (p) (void)hipFree(p);
+    }
+};
+
+modem_status modem_fir_create(const float* taps, uint32_t ntaps, int device, modem_fir** out) {
+    // FIRFilter::new(&[]) would divide by zero in add() (fir.rs:31): reject it here.
+    if (!out || !taps || ntaps < 1 || ntaps > (uint32_t)mk::kMaxTaps) return MODEM_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_fir* h = new (std::nothrow) modem_fir;
+    if (!h) return MODEM_ERR_ALLOC;
+    h->device = device;
+    h->L = ntaps;
+    modem_status st;
+    if ((st = dalloc(&h->d_taps, ntaps)) || (st = dalloc(&h->d_hist[0], ntaps)) ||
+        (st = dalloc(&h->d_hist[1], ntaps))) { delete h; return st; }
+    if (hipMemcpy(h->d_taps, taps, ntaps * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
+    }
+    *out = h;
+    return MODEM_OK;
+}
+
+modem_status modem_fir_process(modem_fir* h, const float* in, float* out, size_t n, void* stream) {
+    if (!h || (n && (!in || !out))) return MODEM_ERR_INVALID_ARG;
+    DeviceGuard g(h->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    hipStream_t s = (hipStream_t)stream;
+    modem_status st;
+    const float* din = in;
+    float* dout = out;
+    if (n && !is_device_ptr(in)) {
+        if ((st = h->in_stage.ensure(n * sizeof(float)))) return st;
+        HIP_TRY(hipMemcpyAsync(h->in_stage.p, in, n * sizeof(float), hipMemcpyHostToDevice, s));
+        din = static_cast<const float*>(h->in_stage.p);
+    }
+    const bool host_out = n && !is_device_ptr(out);
+    if (host_out) {
+        if ((st = h->out_stage.ensure(n * sizeof(float)))) return st;
+        dout = static_cast<float*>(h->out_stage.p);
+    }
+    mk::FirParams p{};
+    p.x = din;
+    p.hist = h->d_hist[h->hcur];
+    p.hist_new = h->d_hist[h->hcur ^ 1];
+    p.y = dout;
+    p.taps = h->d_taps;
+    p.N = (int64_t)n;
+    p.L = (int)h->L;
+    HIP_TRY(mk::launch_fir(p, s));
+    h->hcur ^= 1;
+    if (host_out) HIP_TRY(hipMemcpyAsync(out, dout, n * sizeof(float), hipMemcpyDeviceToHost, s));
+    if (host_out || din != in) HIP_TRY(hipStreamSynchronize(s));
+    return MODEM_OK;
+}
+
+modem_status modem_fir_destroy(modem_fir* h) { delete h; return MODEM_OK; }
+
+modem_status modem_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, int device, void* stream) {
+    if (nbits && !out) return MODEM_ERR_INVALID_ARG;
+    if (nbits && !is_device_ptr(out)) return MODEM_ERR_INVALID_ARG;
+    if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
+    DeviceGuard g(device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    HIP_TRY(mk::launch_prng_bits(seed, out, nbits, (hipStream_t)stream));
+    return MODEM_OK;
+}
+
+}  // extern "C"

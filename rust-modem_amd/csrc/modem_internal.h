@@ -1,0 +1,86 @@
+// rust-modem_amd/csrc/modem_internal.h — kernel parameter blocks and launchers shared by
+// modem_kernels.hip (device code) and modem_capi.cpp (the C ABI). Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mk {
+
+// One TX launch: symbols [0, nsym) of this call -> samples [0, nsym*sps).
+struct TxParams {
+    const uint8_t* bits;     // this call's bits, one byte per bit (device)
+    const uint8_t* carry;    // ncarry leftover bits of the previous call (device)
+    uint8_t* carry_new;      // leftover bits after this call (other buffer)
+    const float2* hist;      // K-1 complex symbol values preceding symbol 0 (device)
+    float2* hist_new;        // K-1 values preceding the next call's symbol 0
+    const float2* lut;       // 2^bps complex points (device)
+    const float* taps;       // polyphase taps, taps[t*sps + p] = h[p + sps*t], K*sps floats
+    void* out;               // f32 or f16 samples (layout per out_mode)
+    uint64_t s0;             // carrier sample of output sample 0
+    int64_t nsym;            // symbols this call emits
+    int64_t nsym_valid;      // symbols < nsym_valid are data, the rest are zero (flush)
+    int64_t nbits;           // bits in `bits`
+    int32_t ncarry;          // bits in `carry`
+    int32_t ncarry_new;      // bits to leave in `carry_new`
+    int32_t update_carry;    // 0 during flush
+    int32_t bps;
+    int32_t sps;             // runtime samples/symbol (generic kernel)
+    int32_t K;               // taps per polyphase branch = ceil(ntaps / sps)
+    int32_t fast_bits;       // ncarry == 0, bps in {1,2,4,8}, bits aligned to bps bytes
+    int32_t small_n;         // every carrier index of this call is < 2^32
+    float w;                 // Freq::sample_freq()
+};
+
+// One RX launch: input samples [0, N) (stream indices n_start ..), outputs k_first ..
+struct RxParams {
+    const void* x;           // this chunk: N complex samples (f32x2 or f16x2)
+    const void* hist;        // HL samples preceding x (same dtype); zeros before the stream
+    void* hist_new;          // HL samples preceding the next chunk
+    void* out_iq;            // decimated filter outputs (f32x2 or f16x2), may be null
+    uint8_t* out_sym;        // decisions, may be null
+    const float* taps;       // polyphase taps, taps[b*K + t] = h[b + decim*t], decim*K floats
+    const float2* slut;      // NEAREST slicer LUT (device)
+    int64_t N;
+    int64_t n_start;         // stream index of x[0]
+    uint64_t c0;             // carrier sample of stream index 0
+    int64_t k_first;         // first kept instant: n = k*decim + D
+    int64_t nout;            // kept instants in this call
+    int32_t K;               // taps per polyphase branch
+    int32_t L;               // ntaps (generic kernel)
+    int32_t HL;              // history length = K*decim - 1
+    int32_t D;               // decim_offset
+    int32_t decim;           // runtime decimation (generic kernel)
+    int32_t x_aligned16;     // x is 16-byte aligned (pair loads)
+    int32_t small_n;
+    int32_t slicer_kind;
+    int32_t bps;
+    int32_t bits_per_carrier;
+    float inv_scale;
+    float max_symbol;
+    float w;
+};
+
+struct FirParams {
+    const float* x;
+    const float* hist;       // L-1 samples preceding x
+    float* hist_new;
+    float* y;
+    const float* taps;       // h[k], L floats
+    int64_t N;
+    int32_t L;
+};
+
+// Launchers return hipSuccess or the launch error. They pick a specialised kernel for the
+// common samples-per-symbol values and a generic one otherwise.
+hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s);
+hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,
+                     hipStream_t s);
+hipError_t launch_fir(const FirParams& p, hipStream_t s);
+hipError_t launch_phases(float w, uint64_t s0, size_t n, float* out, hipStream_t s);
+hipError_t launch_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, hipStream_t s);
+
+// Largest tap count the kernels accept (LDS budget).
+constexpr int kMaxTaps = 4096;
+
+}  // namespace mk

@@ -1,0 +1,718 @@
+// rust-modem_amd/csrc/modem_kernels.hip — gfx950 kernels for the modem sample path.
+//
+// TX  (modulator.rs:64-101 + fir.rs:18-34 + modulator.rs:45-48)
+//   tx_fast<SPS>: one workgroup = TS = 256*R symbols.
+//     1. stage the TS + K - 1 symbols it needs (bits -> bytes_to_bits index -> LUT) in LDS
+//        (digital/util.rs:5-11, the phasor's i()/q() as a precomputed table);
+//     2. each lane computes R consecutive symbols x SPS phases of the zero-stuffed
+//        polyphase FIR  y[m*SPS+p] = sum_t h[p+SPS*t] * a[m-t]  with a sliding register
+//        window (one ds_read_b64 per R*SPS complex MACs; taps are wave-uniform s_loads);
+//     3. transposes the tile through LDS and, per pair of consecutive samples, computes the
+//        bit-exact carrier phase (carrier.rs:17-19, util.rs:3-6), mixes (i+jq)e^{j phase}
+//        and writes 16-B coalesced stores.
+// RX  (demodulator.rs:44-56 + fir.rs:18-34, evaluated only at the kept instants)
+//   rx_fast<DEC>: one workgroup = TS = 256*R output symbols.
+//     1. streams the (TS+K-1)*DEC input samples it needs with 16-B loads, applies the
+//        conjugate (or the reference's real) mix per sample and scatters them into DEC
+//        polyphase planes in LDS  z_b[m] = z[m*DEC + D - b];
+//     2. each lane computes R consecutive outputs  r_k = sum_b sum_t h[b+DEC*t] z_b[k-t]
+//        with one sliding window per plane (ds_read_b64 per R complex MACs);
+//     3. hard decision + store.
+// Both kernels fold the streaming-state update (filter history, leftover bits) into
+// workgroup 0, writing the *other* half of a double buffer, so a call is one launch.
+#include "modem_internal.h"
+
+#include <hip/hip_fp16.h>
+
+namespace mk {
+
+// ----------------------------------------------------------------------------------------
+// Bit-exact reference carrier phase: mod_trig(w * (n as f32)).
+//   x = fl(w * fl(n)); phase = fl(x - fl(TWO_PI * floor(fl(x / TWO_PI)))).
+// fl(x / TWO_PI) is replaced by q1 = q0 + r*RC (q0 = x*RC, r = fma(-q0, TWO_PI, x)):
+// q1 differs from the IEEE quotient for some x but floor(q1) == floor(fl(x/TWO_PI)) for
+// every non-negative finite f32 (checked exhaustively on the host: tests/test_phase_math.py),
+// so the phase is bit-identical. contract(off) keeps TWO_PI*f and the subtraction
+// separately rounded, as rustc does.
+constexpr float kTwoPi = 0x1.921fb6p+2f;   // std::f32::consts::PI * 2.0 (0x40c90fdb)
+constexpr float kRcp2Pi = 0x1.45f306p-3f;  // fl(1 / kTwoPi)
+
+__device__ __forceinline__ float phase_from_f(float w, float nf) {
+#pragma clang fp contract(off)
+    const float x = w * nf;
+    const float q0 = x * kRcp2Pi;
+    const float r = __builtin_fmaf(-q0, kTwoPi, x);
+    const float q1 = __builtin_fmaf(r, kRcp2Pi, q0);
+    const float f = __builtin_floorf(q1);
+    const float p = kTwoPi * f;
+    return x - p;
+}
+
+// `n as f32` with round-to-nearest-even: one v_cvt_f32_u32 below 2^32, the compiler's
+// exact u64 -> f32 sequence above.
+__device__ __forceinline__ float carrier_phase(float w, uint64_t n, bool small_n) {
+    const float nf = small_n ? (float)(uint32_t)n : (float)n;
+    return phase_from_f(w, nf);
+}
+
+// sin/cos of a phase in [0, 2pi]. MODEM_PRECISE_TRIG selects a Cody-Waite + minimax
+// polynomial (<= 2 ulp); the default uses the hardware v_sin_f32/v_cos_f32 (input in
+// revolutions). Either way the sample tolerance is set in tests/test_gpu_parity.py.
+__device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
+#ifdef MODEM_PRECISE_TRIG
+    const float j = __builtin_rintf(ph * 0.63661977236758134f);
+    float r = __builtin_fmaf(-j, 1.57079637050628662f, ph);
+    r = __builtin_fmaf(-j, -4.37113900018624283e-8f, r);
+    const float r2 = r * r;
+    float sp = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+    sp = __builtin_fmaf(r2, sp, -1.6666654611e-1f);
+    const float sr = __builtin_fmaf(r * r2, sp, r);
+    float cp = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    cp = __builtin_fmaf(r2, cp, 4.166664568298827e-2f);
+    const float cr = __builtin_fmaf(r2 * r2, cp, __builtin_fmaf(-0.5f, r2, 1.0f));
+    const int q = (int)j & 3;
+    const float ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+#else
+    s = __sinf(ph);
+    c = __cosf(ph);
+#endif
+}
+
+typedef const __attribute__((address_space(4))) float cfloat;   // wave-uniform -> s_load
+
+// ---------------------------------------------------------------- symbol mapping (TX) ----
+// bytes_to_bits (digital/util.rs:5-11) of symbol m's bits, MSB first, `b & 1` per byte.
+__device__ __forceinline__ uint32_t tx_symbol_index(const TxParams& p, int64_t m) {
+    const int bps = p.bps;
+    if (p.fast_bits) {
+        const uint8_t* b = p.bits + m * bps;
+        if (bps == 4) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(b);
+            return ((v & 1u) << 3) | ((v >> 6) & 4u) | ((v >> 15) & 2u) | ((v >> 24) & 1u);
+        }
+        if (bps == 2) {
+            const uint32_t v = *reinterpret_cast<const uint16_t*>(b);
+            return ((v & 1u) << 1) | ((v >> 8) & 1u);
+        }
+        if (bps == 1) return b[0] & 1u;
+        if (bps == 8) {
+            const uint64_t v = *reinterpret_cast<const uint64_t*>(b);
+            uint32_t idx = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) idx |= (uint32_t)((v >> (8 * q)) & 1u) << (7 - q);
+            return idx;
+        }
+    }
+    uint32_t idx = 0;
+    const int64_t l0 = m * bps;
+    for (int q = 0; q < bps; ++q) {
+        const int64_t l = l0 + q;   // logical bit position in [carry | bits]
+        const uint8_t b = l < p.ncarry ? p.carry[l] : p.bits[l - p.ncarry];
+        idx = (idx << 1) | (b & 1u);
+    }
+    return idx;
+}
+
+__device__ __forceinline__ float2 tx_symbol_value(const TxParams& p, int64_t m) {
+    if (m < 0) return p.hist[m + p.K - 1];
+    if (m >= p.nsym_valid) return make_float2(0.f, 0.f);
+    return p.lut[tx_symbol_index(p, m)];
+}
+
+// Streaming state for the next call, written by workgroup 0 into the other buffers.
+__device__ void tx_state_update(const TxParams& p) {
+    for (int i = threadIdx.x; i < p.K - 1; i += blockDim.x)
+        p.hist_new[i] = tx_symbol_value(p, p.nsym - (p.K - 1) + i);
+    if (p.update_carry) {
+        for (int i = threadIdx.x; i < p.ncarry_new; i += blockDim.x) {
+            const int64_t l = p.nsym * p.bps + i;
+            p.carry_new[i] = l < p.ncarry ? p.carry[l] : p.bits[l - p.ncarry];
+        }
+    }
+}
+
+template <typename OutT> struct OutIO;
+template <> struct OutIO<float> {
+    __device__ static void store_pair(void* out, int64_t j, float a, float b, float c, float d) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + 2 * j) = make_float4(a, b, c, d);
+    }
+    __device__ static void store_one(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + 2 * j) = make_float2(a, b);
+    }
+    __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + j) = make_float2(a, b);
+    }
+    __device__ static void store_real_one(void* out, int64_t j, float a) {
+        reinterpret_cast<float*>(out)[j] = a;
+    }
+};
+template <> struct OutIO<__half> {
+    __device__ static void store_pair(void* out, int64_t j, float a, float b, float c, float d) {
+        const __half2 h0 = __floats2half2_rn(a, b), h1 = __floats2half2_rn(c, d);
+        uint2 u;
+        u.x = *reinterpret_cast<const uint32_t*>(&h0);
+        u.y = *reinterpret_cast<const uint32_t*>(&h1);
+        *reinterpret_cast<uint2*>(reinterpret_cast<__half*>(out) + 2 * j) = u;
+    }
+    __device__ static void store_one(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + 2 * j) = __floats2half2_rn(a, b);
+    }
+    __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + j) = __floats2half2_rn(a, b);
+    }
+    __device__ static void store_real_one(void* out, int64_t j, float a) {
+        reinterpret_cast<__half*>(out)[j] = __float2half_rn(a);
+    }
+};
+
+enum { OUT_IQ_MIXED = 0, OUT_IQ_BASEBAND = 1, OUT_REAL = 2 };
+
+// Mix one filtered baseband sample onto the carrier (IQSample::modulate, modulator.rs:45-48).
+template <int OUT_MODE>
+__device__ __forceinline__ float2 tx_mix(float w, uint64_t n, bool small_n, float2 y) {
+    if (OUT_MODE == OUT_IQ_BASEBAND) return y;
+    float s, c;
+    sincos_phase(carrier_phase(w, n, small_n), s, c);
+    return make_float2(y.x * c - y.y * s, y.x * s + y.y * c);
+}
+
+template <int OUT_MODE, typename OutT>
+__device__ __forceinline__ void tx_emit(const TxParams& p, int64_t j, float2 y0, float2 y1,
+                                        bool two) {
+    const uint64_t n = p.s0 + (uint64_t)j;
+    const float2 z0 = tx_mix<OUT_MODE>(p.w, n, p.small_n, y0);
+    if (two) {
+        const float2 z1 = tx_mix<OUT_MODE>(p.w, n + 1, p.small_n, y1);
+        if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_pair(p.out, j, z0.x, z1.x);
+        else OutIO<OutT>::store_pair(p.out, j, z0.x, z0.y, z1.x, z1.y);
+    } else {
+        if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, j, z0.x);
+        else OutIO<OutT>::store_one(p.out, j, z0.x, z0.y);
+    }
+}
+
+template <int SPS> struct TxCfg {
+    static constexpr int R = SPS == 1 ? 15 : SPS == 2 ? 9 : SPS == 4 ? 5 : SPS == 8 ? 3 : 1;
+    static constexpr int NT = 256;
+    static constexpr int TS = NT * R;   // symbols per workgroup
+    static constexpr int CH = 8;        // taps unrolled per loop trip
+};
+
+template <int SPS, int R>
+__device__ __forceinline__ void tx_mac(float (&ar)[R][SPS], float (&ai)[R][SPS],
+                                       const float2 (&win)[R], cfloat* h) {
+    float hv[SPS];
+#pragma unroll
+    for (int q = 0; q < SPS; ++q) hv[q] = h[q];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < SPS; ++q) {
+            ar[r][q] = __builtin_fmaf(win[r].x, hv[q], ar[r][q]);
+            ai[r][q] = __builtin_fmaf(win[r].y, hv[q], ai[r][q]);
+        }
+}
+
+template <int R>
+__device__ __forceinline__ void shift_in(float2 (&win)[R], float2 v) {
+#pragma unroll
+    for (int r = R - 1; r > 0; --r) win[r] = win[r - 1];
+    win[0] = v;
+}
+
+template <int SPS, int OUT_MODE, typename OutT>
+__global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
+    using C = TxCfg<SPS>;
+    constexpr int R = C::R, NT = C::NT, TS = C::TS, CH = C::CH;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int tid = threadIdx.x;
+    const int K = p.K;
+    if (blockIdx.x == 0) tx_state_update(p);
+    const int64_t m0 = (int64_t)blockIdx.x * TS;
+    if (m0 >= p.nsym) return;   // workgroup-uniform
+
+    // 1. symbols m0-(K-1) .. m0+TS-1 -> lds[1 ..]; lds[0] is a pad for the last shift-in.
+    for (int e = tid; e < TS + K - 1; e += NT) lds[1 + e] = tx_symbol_value(p, m0 - (K - 1) + e);
+    __syncthreads();
+
+    // 2. polyphase FIR, R symbols x SPS phases per lane.
+    float ar[R][SPS], ai[R][SPS];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < SPS; ++q) { ar[r][q] = 0.f; ai[r][q] = 0.f; }
+    const float2* base = lds + 1 + tid * R + (K - 1);   // base[j] = a[m0 + tid*R + j]
+    float2 win[R];                                      // win[r] = a[m + r - t]
+#pragma unroll
+    for (int r = 0; r < R; ++r) win[r] = base[r];
+    cfloat* taps = (cfloat*)p.taps;
+    int t = 0;
+    for (; t + CH <= K; t += CH) {
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            tx_mac<SPS, R>(ar, ai, win, taps + (t + c) * SPS);
+            shift_in<R>(win, base[-(t + c + 1)]);
+        }
+    }
+    for (; t < K; ++t) {
+        tx_mac<SPS, R>(ar, ai, win, taps + t * SPS);
+        shift_in<R>(win, base[-(t + 1)]);
+    }
+    __syncthreads();
+
+    // 3. tile transpose: lane-blocked samples -> LDS -> consecutive pairs per lane.
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int q = 0; q < SPS; ++q)
+            lds[(tid * R + r) * SPS + q] = make_float2(ar[r][q], ai[r][q]);
+    __syncthreads();
+    const int64_t nsym_here = p.nsym - m0 < TS ? p.nsym - m0 : TS;
+    const int nsamp = (int)nsym_here * SPS;
+    const int64_t j0 = m0 * SPS;
+    for (int i = 2 * tid; i < nsamp; i += 2 * NT) {
+        const bool two = i + 1 < nsamp;
+        tx_emit<OUT_MODE, OutT>(p, j0 + i, lds[i], two ? lds[i + 1] : make_float2(0.f, 0.f), two);
+    }
+}
+
+// Any samples-per-symbol: thread per output sample, symbols staged in LDS.
+template <int OUT_MODE, typename OutT>
+__global__ __launch_bounds__(256) void tx_generic(const TxParams p) {
+    constexpr int NT = 256, TS = 64;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int K = p.K, SPS = p.sps;
+    if (blockIdx.x == 0) tx_state_update(p);
+    const int64_t m0 = (int64_t)blockIdx.x * TS;
+    if (m0 >= p.nsym) return;
+    for (int e = threadIdx.x; e < TS + K - 1; e += NT) lds[e] = tx_symbol_value(p, m0 - (K - 1) + e);
+    __syncthreads();
+    const int64_t nsym_here = p.nsym - m0 < TS ? p.nsym - m0 : TS;
+    const int nsamp = (int)nsym_here * SPS;
+    for (int i = threadIdx.x; i < nsamp; i += NT) {
+        const int ml = i / SPS, q = i - ml * SPS;
+        float yr = 0.f, yi = 0.f;
+        for (int t = 0; t < K; ++t) {
+            const float h = p.taps[t * SPS + q];
+            const float2 a = lds[ml - t + K - 1];
+            yr = __builtin_fmaf(a.x, h, yr);
+            yi = __builtin_fmaf(a.y, h, yi);
+        }
+        tx_emit<OUT_MODE, OutT>(p, m0 * SPS + i, make_float2(yr, yi), make_float2(0.f, 0.f), false);
+    }
+}
+
+// -------------------------------------------------------------------------------- RX ----
+template <typename InT> struct InIO;
+template <> struct InIO<float> {
+    __device__ static float2 load(const void* x, int64_t q) {
+        return reinterpret_cast<const float2*>(x)[q];
+    }
+    __device__ static void load_pair(const void* x, int64_t q, float2& a, float2& b) {
+        const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(x) + q);
+        a = make_float2(v.x, v.y);
+        b = make_float2(v.z, v.w);
+    }
+    __device__ static void copy(void* dst, int64_t i, const void* src, int64_t q) {
+        reinterpret_cast<float2*>(dst)[i] = reinterpret_cast<const float2*>(src)[q];
+    }
+};
+template <> struct InIO<__half> {
+    __device__ static float2 load(const void* x, int64_t q) {
+        return __half22float2(reinterpret_cast<const __half2*>(x)[q]);
+    }
+    __device__ static void load_pair(const void* x, int64_t q, float2& a, float2& b) {
+        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half2*>(x) + q);
+        a = __half22float2(*reinterpret_cast<const __half2*>(&u.x));
+        b = __half22float2(*reinterpret_cast<const __half2*>(&u.y));
+    }
+    __device__ static void copy(void* dst, int64_t i, const void* src, int64_t q) {
+        reinterpret_cast<__half2*>(dst)[i] = reinterpret_cast<const __half2*>(src)[q];
+    }
+};
+
+enum { MIX_COMPLEX = 0, MIX_REFERENCE_REAL = 1 };
+enum { SLICER_NONE = 0, SLICER_NEAREST = 1, SLICER_QAM_AXIS = 2 };
+
+// Sample q of the chunk (q < 0: history; q >= N: past the chunk, zero).
+template <typename InT>
+__device__ __forceinline__ float2 rx_sample(const RxParams& p, int64_t q) {
+    if (q >= 0) return q < p.N ? InIO<InT>::load(p.x, q) : make_float2(0.f, 0.f);
+    return InIO<InT>::load(p.hist, q + p.HL);
+}
+
+template <typename InT>
+__device__ __forceinline__ void rx_pair(const RxParams& p, int64_t q, float2& a, float2& b) {
+    if (q >= 0 && q + 1 < p.N && p.x_aligned16) {
+        InIO<InT>::load_pair(p.x, q, a, b);
+    } else {
+        a = rx_sample<InT>(p, q);
+        b = rx_sample<InT>(p, q + 1);
+    }
+}
+
+// x * e^{-j phase} (or the reference's x.re * (cos, -sin), demodulator.rs:46,53-54).
+template <int MIX>
+__device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t n, float2 x) {
+    if (n < 0) return make_float2(0.f, 0.f);   // before the stream: zero history
+    float s, c;
+    sincos_phase(carrier_phase(p.w, p.c0 + (uint64_t)n, p.small_n), s, c);
+    if (MIX == MIX_REFERENCE_REAL) return make_float2(x.x * c, x.x * -s);
+    return make_float2(__builtin_fmaf(x.y, s, x.x * c), __builtin_fmaf(-x.x, s, x.y * c));
+}
+
+__device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    if (p.slicer_kind == SLICER_QAM_AXIS) {
+        const int ms = (int)p.max_symbol;
+        const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
+        const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
+        int si = (int)__builtin_rintf(fi), sq = (int)__builtin_rintf(fq);
+        si = si < 0 ? 0 : (si > ms ? ms : si);
+        sq = sq < 0 ? 0 : (sq > ms ? ms : sq);
+        return (uint8_t)((si << p.bits_per_carrier) | sq);
+    }
+    cfloat* lut = (cfloat*)p.slut;
+    const int n = 1 << p.bps;
+    uint32_t best = 0;
+    float bd = __builtin_inff();
+    for (int k = 0; k < n; ++k) {
+        const float dr = re - lut[2 * k], di = im - lut[2 * k + 1];
+        const float d = dr * dr + di * di;
+        if (d < bd) { bd = d; best = (uint32_t)k; }
+    }
+    return (uint8_t)best;
+}
+
+template <typename OutT>
+__device__ __forceinline__ void rx_emit(const RxParams& p, int64_t o, float re, float im) {
+    if (p.out_iq) OutIO<OutT>::store_one(p.out_iq, o, re, im);
+    if (p.out_sym && p.slicer_kind != SLICER_NONE) p.out_sym[o] = rx_slice(p, re, im);
+}
+
+template <typename InT>
+__device__ void rx_state_update(const RxParams& p) {
+    for (int i = threadIdx.x; i < p.HL; i += blockDim.x) {
+        const int64_t q = p.N - p.HL + i;
+        if (q >= 0) InIO<InT>::copy(p.hist_new, i, p.x, q);
+        else InIO<InT>::copy(p.hist_new, i, p.hist, q + p.HL);
+    }
+}
+
+template <int DEC> struct RxCfg {
+    static constexpr int R = DEC == 1 ? 9 : DEC == 2 ? 7 : DEC == 4 ? 5 : DEC == 8 ? 3 : 1;
+    static constexpr int NT = 256;
+    static constexpr int TS = NT * R;   // output symbols per workgroup
+    static constexpr int CH = 8;
+};
+
+template <int R>
+__device__ __forceinline__ void rx_mac(float (&ar)[R], float (&ai)[R], const float2 (&win)[R],
+                                       float h) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        ar[i] = __builtin_fmaf(win[i].x, h, ar[i]);
+        ai[i] = __builtin_fmaf(win[i].y, h, ai[i]);
+    }
+}
+
+// Plane stride (float2 elements): TS + K rounded to an odd count (bank spread of the
+// per-plane base); lanes read with stride R (odd) -> conflict-free ds_read_b64.
+__host__ __device__ inline int rx_plane_stride(int TS, int K) { return (TS + K) | 1; }
+
+template <int DEC, typename InT, int MIX, typename OutT>
+__global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
+    using C = RxCfg<DEC>;
+    constexpr int R = C::R, NT = C::NT, TS = C::TS, CH = C::CH;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int tid = threadIdx.x;
+    const int K = p.K;
+    const int PS = rx_plane_stride(TS, K);
+    if (blockIdx.x == 0) rx_state_update<InT>(p);
+    const int64_t k0 = p.k_first + (int64_t)blockIdx.x * TS;
+    if ((int64_t)blockIdx.x * TS >= p.nout) return;   // workgroup-uniform
+
+    // 1. samples n_lo .. n_lo + NS - 1 (stream indices), mixed, into planes:
+    //    sample e -> plane b = DEC-1 - e%DEC, index e/DEC   (z_b[m] = z[m*DEC + D - b]).
+    const int64_t n_lo = k0 * DEC + p.D - (int64_t)K * DEC + 1;
+    const int64_t q_lo = n_lo - p.n_start;
+    const int NS = (TS + K - 1) * DEC;
+    const int par = (int)(q_lo & 1);
+    for (int e = 2 * tid - par; e < NS; e += 2 * NT) {
+        float2 x0, x1;
+        rx_pair<InT>(p, q_lo + e, x0, x1);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int eu = e + u;
+            if (eu < 0 || eu >= NS) continue;
+            const float2 z = rx_mix<MIX>(p, n_lo + eu, u ? x1 : x0);
+            const int em = eu / DEC, b = DEC - 1 - (eu - em * DEC);
+            lds[b * PS + 1 + em] = z;
+        }
+    }
+    __syncthreads();
+
+    // 2. matched filter at the kept instants, R consecutive outputs per lane.
+    float ar[R], ai[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) { ar[i] = 0.f; ai[i] = 0.f; }
+    cfloat* taps = (cfloat*)p.taps;
+#pragma unroll
+    for (int b = 0; b < DEC; ++b) {
+        const float2* base = lds + b * PS + 1 + tid * R + (K - 1);   // base[j] = z_b[k+j]
+        cfloat* hb = taps + b * K;
+        float2 win[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) win[i] = base[i];
+        int t = 0;
+        for (; t + CH <= K; t += CH) {
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                rx_mac<R>(ar, ai, win, hb[t + c]);
+                shift_in<R>(win, base[-(t + c + 1)]);
+            }
+        }
+        for (; t < K; ++t) {
+            rx_mac<R>(ar, ai, win, hb[t]);
+            shift_in<R>(win, base[-(t + 1)]);
+        }
+    }
+
+    // 3. decisions + stores.
+    const float g = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const int64_t o = (int64_t)blockIdx.x * TS + tid * R + i;
+        if (o < p.nout) rx_emit<OutT>(p, o, g * ar[i], g * ai[i]);
+    }
+}
+
+// Any decimation: thread per kept instant, mixed samples staged in natural order.
+template <typename InT, int MIX, typename OutT>
+__global__ __launch_bounds__(64) void rx_generic(const RxParams p) {
+    constexpr int TS = 64;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int L = p.L, DEC = p.decim;
+    if (blockIdx.x == 0) rx_state_update<InT>(p);
+    const int64_t k0 = p.k_first + (int64_t)blockIdx.x * TS;
+    if ((int64_t)blockIdx.x * TS >= p.nout) return;
+    const int64_t n_lo = k0 * DEC + p.D - (L - 1);
+    const int NS = (TS - 1) * DEC + L;
+    for (int e = threadIdx.x; e < NS; e += TS)
+        lds[e] = rx_mix<MIX>(p, n_lo + e, rx_sample<InT>(p, n_lo + e - p.n_start));
+    __syncthreads();
+    const int64_t o = (int64_t)blockIdx.x * TS + threadIdx.x;
+    if (o >= p.nout) return;
+    const int c = threadIdx.x * DEC + L - 1;
+    float yr = 0.f, yi = 0.f;
+    for (int j = 0; j < L; ++j) {
+        const float h = p.taps[(j % DEC) * p.K + j / DEC];
+        yr = __builtin_fmaf(lds[c - j].x, h, yr);
+        yi = __builtin_fmaf(lds[c - j].y, h, yi);
+    }
+    const float g = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
+    rx_emit<OutT>(p, o, g * yr, g * yi);
+}
+
+// ------------------------------------------------------------------- FIRFilter (real) ----
+// y[n] = sum_{k<L} h[k] x[n-k] (fir.rs:18-34); 256 lanes x 16 outputs per workgroup.
+constexpr int kFirR = 16, kFirNT = 256, kFirTS = kFirR * kFirNT;
+
+__global__ __launch_bounds__(256) void fir_real(const FirParams p) {
+    extern __shared__ __attribute__((aligned(16))) float flds[];
+    const int tid = threadIdx.x, L = p.L;
+    if (blockIdx.x == 0)
+        for (int i = tid; i < L - 1; i += kFirNT) {
+            const int64_t q = p.N - (L - 1) + i;
+            p.hist_new[i] = q >= 0 ? p.x[q] : p.hist[q + L - 1];
+        }
+    const int64_t n0 = (int64_t)blockIdx.x * kFirTS;
+    if (n0 >= p.N) return;
+    for (int e = tid; e < kFirTS + L - 1; e += kFirNT) {
+        const int64_t q = n0 - (L - 1) + e;
+        flds[1 + e] = q < 0 ? p.hist[q + L - 1] : (q < p.N ? p.x[q] : 0.f);
+    }
+    __syncthreads();
+    float acc[kFirR];
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r) acc[r] = 0.f;
+    const float* base = flds + 1 + tid * kFirR + (L - 1);
+    float win[kFirR];
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r) win[r] = base[r];
+    cfloat* taps = (cfloat*)p.taps;
+    int k = 0;
+    for (; k + 8 <= L; k += 8) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const float h = taps[k + c];
+#pragma unroll
+            for (int r = 0; r < kFirR; ++r) acc[r] = __builtin_fmaf(win[r], h, acc[r]);
+#pragma unroll
+            for (int r = kFirR - 1; r > 0; --r) win[r] = win[r - 1];
+            win[0] = base[-(k + c + 1)];
+        }
+    }
+    for (; k < L; ++k) {
+        const float h = taps[k];
+#pragma unroll
+        for (int r = 0; r < kFirR; ++r) acc[r] = __builtin_fmaf(win[r], h, acc[r]);
+#pragma unroll
+        for (int r = kFirR - 1; r > 0; --r) win[r] = win[r - 1];
+        win[0] = base[-(k + 1)];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kFirR; ++r) flds[tid * kFirR + r] = acc[r];
+    __syncthreads();
+    const int64_t nh = p.N - n0 < kFirTS ? p.N - n0 : kFirTS;
+    for (int i = tid; i < nh; i += kFirNT) p.y[n0 + i] = flds[i];
+}
+
+// ----------------------------------------------------------- carrier phases (tests) ----
+__global__ __launch_bounds__(256) void carrier_phases(float w, uint64_t s0, size_t n, int small_n,
+                                                      float* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = carrier_phase(w, s0 + i, small_n != 0);
+}
+
+hipError_t launch_phases(float w, uint64_t s0, size_t n, float* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const int small_n = (s0 + n) <= (1ull << 32) ? 1 : 0;
+    hipLaunchKernelGGL(carrier_phases, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, s0, n,
+                       small_n, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------- splitmix64 bits ----
+__global__ __launch_bounds__(256) void prng_bits(uint64_t seed, uint8_t* out, size_t nbits) {
+    const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // one 64-bit word
+    if (w * 64 >= nbits) return;
+    uint64_t z = seed + (uint64_t)(w + 1) * 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z = z ^ (z >> 31);
+    const size_t b0 = w * 64;
+    if (b0 + 64 <= nbits && (reinterpret_cast<uintptr_t>(out + b0) & 15) == 0) {
+        uint4* o = reinterpret_cast<uint4*>(out + b0);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            uint32_t wd[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int bit = v * 16 + k * 4;
+                wd[k] = (uint32_t)((z >> bit) & 1) | (uint32_t)((z >> (bit + 1)) & 1) << 8 |
+                        (uint32_t)((z >> (bit + 2)) & 1) << 16 | (uint32_t)((z >> (bit + 3)) & 1) << 24;
+            }
+            o[v] = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+        }
+    } else {
+        for (size_t i = b0; i < nbits; ++i) out[i] = (uint8_t)((z >> (i - b0)) & 1);
+    }
+}
+
+// ---------------------------------------------------------------------- dispatch ----
+template <int SPS, int OM, typename OutT>
+static hipError_t tx_go(const TxParams& p, hipStream_t s) {
+    using C = TxCfg<SPS>;
+    const int64_t nblk = (p.nsym + C::TS - 1) / C::TS;
+    const size_t a = (size_t)(C::TS + p.K) * sizeof(float2);
+    const size_t b = (size_t)C::TS * SPS * sizeof(float2);
+    const size_t lds = a > b ? a : b;
+    hipLaunchKernelGGL((tx_fast<SPS, OM, OutT>), dim3((unsigned)(nblk > 0 ? nblk : 1)),
+                       dim3(C::NT), lds, s, p);
+    return hipGetLastError();
+}
+
+template <int OM, typename OutT>
+static hipError_t tx_sps(const TxParams& p, int sps, hipStream_t s) {
+    switch (sps) {
+    case 1: return tx_go<1, OM, OutT>(p, s);
+    case 2: return tx_go<2, OM, OutT>(p, s);
+    case 4: return tx_go<4, OM, OutT>(p, s);
+    case 8: return tx_go<8, OM, OutT>(p, s);
+    case 16: return tx_go<16, OM, OutT>(p, s);
+    default: {
+        const int64_t nblk = (p.nsym + 63) / 64;
+        const size_t lds = (size_t)(64 + p.K) * sizeof(float2);
+        hipLaunchKernelGGL((tx_generic<OM, OutT>), dim3((unsigned)(nblk > 0 ? nblk : 1)), dim3(256),
+                           lds, s, p);
+        return hipGetLastError();
+    }
+    }
+}
+
+template <typename OutT>
+static hipError_t tx_mode(const TxParams& p, int sps, int out_mode, hipStream_t s) {
+    switch (out_mode) {
+    case OUT_IQ_MIXED: return tx_sps<OUT_IQ_MIXED, OutT>(p, sps, s);
+    case OUT_IQ_BASEBAND: return tx_sps<OUT_IQ_BASEBAND, OutT>(p, sps, s);
+    default: return tx_sps<OUT_REAL, OutT>(p, sps, s);
+    }
+}
+
+hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s) {
+    return dtype == 1 ? tx_mode<__half>(p, sps, out_mode, s) : tx_mode<float>(p, sps, out_mode, s);
+}
+
+template <int DEC, typename InT, int MIX, typename OutT>
+static hipError_t rx_go(const RxParams& p, hipStream_t s) {
+    using C = RxCfg<DEC>;
+    const int64_t nblk = (p.nout + C::TS - 1) / C::TS;
+    const size_t lds = ((size_t)DEC * rx_plane_stride(C::TS, p.K) + 1) * sizeof(float2);
+    hipLaunchKernelGGL((rx_fast<DEC, InT, MIX, OutT>), dim3((unsigned)(nblk > 0 ? nblk : 1)),
+                       dim3(C::NT), lds, s, p);
+    return hipGetLastError();
+}
+
+template <typename InT, int MIX, typename OutT>
+static hipError_t rx_dec(const RxParams& p, int decim, hipStream_t s) {
+    switch (decim) {
+    case 1: return rx_go<1, InT, MIX, OutT>(p, s);
+    case 2: return rx_go<2, InT, MIX, OutT>(p, s);
+    case 4: return rx_go<4, InT, MIX, OutT>(p, s);
+    case 8: return rx_go<8, InT, MIX, OutT>(p, s);
+    case 16: return rx_go<16, InT, MIX, OutT>(p, s);
+    default: {
+        const int64_t nblk = (p.nout + 63) / 64;
+        const size_t lds = (size_t)(63 * decim + p.L) * sizeof(float2);
+        hipLaunchKernelGGL((rx_generic<InT, MIX, OutT>), dim3((unsigned)(nblk > 0 ? nblk : 1)),
+                           dim3(64), lds, s, p);
+        return hipGetLastError();
+    }
+    }
+}
+
+template <typename InT, typename OutT>
+static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s) {
+    return mix == MIX_REFERENCE_REAL ? rx_dec<InT, MIX_REFERENCE_REAL, OutT>(p, decim, s)
+                                     : rx_dec<InT, MIX_COMPLEX, OutT>(p, decim, s);
+}
+
+hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,
+                     hipStream_t s) {
+    if (in_dtype == 1)
+        return out_dtype == 1 ? rx_mixsel<__half, __half>(p, decim, mix, s)
+                              : rx_mixsel<__half, float>(p, decim, mix, s);
+    return out_dtype == 1 ? rx_mixsel<float, __half>(p, decim, mix, s)
+                          : rx_mixsel<float, float>(p, decim, mix, s);
+}
+
+hipError_t launch_fir(const FirParams& p, hipStream_t s) {
+    const int64_t nblk = (p.N + kFirTS - 1) / kFirTS;
+    const size_t lds = (size_t)(kFirTS + p.L + 1) * sizeof(float);
+    hipLaunchKernelGGL(fir_real, dim3((unsigned)(nblk > 0 ? nblk : 1)), dim3(kFirNT), lds, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, hipStream_t s) {
+    const size_t words = (nbits + 63) / 64;
+    const size_t nblk = (words + 255) / 256;
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(prng_bits, dim3((unsigned)nblk), dim3(256), 0, s, seed, out, nbits);
+    return hipGetLastError();
+}
+
+}  // namespace mk
