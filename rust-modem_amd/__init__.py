@@ -114,6 +114,14 @@ def load_library():
     if not os.path.exists(path):
         _lib_err = f"{path} not built (run __graft_entry__.build() or `make -C rust-modem_amd`)"
         raise ModemError(ERR_UNSUPPORTED, _lib_err)
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7,
+    # loaded by its NEEDED name "libamdhip64.so"). Loading torch first lets our NEEDED
+    # libamdhip64.so.7 resolve to that already-loaded runtime, so device pointers and
+    # streams from torch are valid here. Without torch, /opt/rocm's runtime is used.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     c = ctypes
     vp, sz, u64, u32, f32, st = c.c_void_p, c.c_size_t, c.c_uint64, c.c_uint32, c.c_float, c.c_int
