@@ -522,14 +522,17 @@ class DemodulatorRx:
         a, b = first(self._consumed), first(self._consumed + n)
         return max(0, b - a)
 
-    def process(self, iq, want_iq: bool = True, want_sym: bool = True, stream=None):
+    def process(self, iq, want_iq: bool = True, want_sym: bool = True, stream=None,
+                out_iq=None, out_sym=None):
         n = int(iq.shape[0])
         nout = self.noutputs(n)
         npd = np.float16 if self.out_dtype == DTYPE_F16 else np.float32
-        oiq = _empty_like_input(iq, (nout, 2), npd) if want_iq else None
-        osym = _empty_like_input(iq, (nout,), np.uint8) if (want_sym and self._slicer is not None) else None
+        oiq = out_iq if out_iq is not None else (_empty_like_input(iq, (nout, 2), npd) if want_iq else None)
+        osym = out_sym if out_sym is not None else (
+            _empty_like_input(iq, (nout,), np.uint8) if (want_sym and self._slicer is not None) else None)
+        cap = min(int(oiq.shape[0]) if oiq is not None else nout, int(osym.shape[0]) if osym is not None else nout)
         prod = ctypes.c_size_t()
-        _check(load_library().modem_rx_process(self._h, _ptr(iq), n, _ptr(oiq), _ptr(osym), nout,
+        _check(load_library().modem_rx_process(self._h, _ptr(iq), n, _ptr(oiq), _ptr(osym), cap,
                                                ctypes.byref(prod), _stream_handle(stream)),
                "Demodulator.process")
         self._consumed += n

@@ -24,6 +24,10 @@
 
 #include <hip/hip_fp16.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 namespace mk {
 
 // ----------------------------------------------------------------------------------------
@@ -55,6 +59,12 @@ __device__ __forceinline__ float carrier_phase(float w, uint64_t n, bool small_n
     return phase_from_f(w, nf);
 }
 
+// Same, for n = base + off with a wave-uniform 64-bit base and a 32-bit lane offset.
+__device__ __forceinline__ float carrier_phase_off(float w, uint64_t base, int off, bool small_n) {
+    const float nf = small_n ? (float)((uint32_t)base + (uint32_t)off) : (float)(base + (int64_t)off);
+    return phase_from_f(w, nf);
+}
+
 // sin/cos of a phase in [0, 2pi]. MODEM_PRECISE_TRIG selects a Cody-Waite + minimax
 // polynomial (<= 2 ulp); the default uses the hardware v_sin_f32/v_cos_f32 (input in
 // revolutions). Either way the sample tolerance is set in tests/test_gpu_parity.py.
@@ -81,6 +91,12 @@ __device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
 }
 
 typedef const __attribute__((address_space(4))) float cfloat;   // wave-uniform -> s_load
+// (re, im) pair: one v_pk_fma_f32 per complex x real MAC, tap broadcast from an SGPR.
+typedef float cf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ cf2 ldc(const float2* p) { return *reinterpret_cast<const cf2*>(p); }
+__device__ __forceinline__ cf2 cmac(cf2 x, float h, cf2 acc) {
+    return __builtin_elementwise_fma(x, (cf2){h, h}, acc);
+}
 
 // ---------------------------------------------------------------- symbol mapping (TX) ----
 // bytes_to_bits (digital/util.rs:5-11) of symbol m's bits, MSB first, `b & 1` per byte.
@@ -194,29 +210,51 @@ __device__ __forceinline__ void tx_emit(const TxParams& p, int64_t j, float2 y0,
 }
 
 template <int SPS> struct TxCfg {
-    static constexpr int R = SPS == 1 ? 15 : SPS == 2 ? 9 : SPS == 4 ? 5 : SPS == 8 ? 3 : 1;
+    // R consecutive symbols per lane -> R*SPS consecutive output samples per lane
+    // (R*SPS*8 B, so a store instruction touches 64-B pieces of 16-32 lines).
+    static constexpr int R = SPS == 1 ? 8 : SPS == 2 ? 4 : SPS == 4 ? 2 : 1;
     static constexpr int NT = 256;
-    static constexpr int TS = NT * R;   // symbols per workgroup
-    static constexpr int CH = 8;        // taps unrolled per loop trip
+    static constexpr int TS = NT * R;            // symbols per tile
+    static constexpr int CH = 8;                 // taps unrolled per loop trip
+    static constexpr int U = (TS + NT) / NT;     // staging slots prefetched per lane
 };
 
+// Raw bits word of symbol m (fast path: one aligned 1/2/4/8-byte load). The address is
+// clamped so the load is unconditional (no per-element branch around it); symbols outside
+// [0, nsym_valid) are fixed up when staged.
+__device__ __forceinline__ uint64_t tx_load_word(const TxParams& p, int64_t m) {
+    const int64_t mc = m < 0 ? 0 : (m >= p.nsym_valid ? p.nsym_valid - 1 : m);
+    const uint8_t* b = p.bits + mc * p.bps;
+    switch (p.bps) {
+    case 1: return *b;
+    case 2: return *reinterpret_cast<const uint16_t*>(b);
+    case 4: return *reinterpret_cast<const uint32_t*>(b);
+    default: return *reinterpret_cast<const uint64_t*>(b);
+    }
+}
+
+// bytes_to_bits (digital/util.rs:5-11) of a little-endian word holding bps bytes.
+__device__ __forceinline__ uint32_t word_index(uint64_t v, int bps) {
+    uint32_t idx = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if (q < bps) idx |= (uint32_t)((v >> (8 * q)) & 1u) << (bps - 1 - q);
+    return idx;
+}
+
 template <int SPS, int R>
-__device__ __forceinline__ void tx_mac(float (&ar)[R][SPS], float (&ai)[R][SPS],
-                                       const float2 (&win)[R], cfloat* h) {
+__device__ __forceinline__ void tx_mac(cf2 (&acc)[R][SPS], const cf2 (&win)[R], cfloat* h) {
     float hv[SPS];
 #pragma unroll
     for (int q = 0; q < SPS; ++q) hv[q] = h[q];
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int q = 0; q < SPS; ++q) {
-            ar[r][q] = __builtin_fmaf(win[r].x, hv[q], ar[r][q]);
-            ai[r][q] = __builtin_fmaf(win[r].y, hv[q], ai[r][q]);
-        }
+        for (int q = 0; q < SPS; ++q) acc[r][q] = cmac(win[r], hv[q], acc[r][q]);
 }
 
 template <int R>
-__device__ __forceinline__ void shift_in(float2 (&win)[R], float2 v) {
+__device__ __forceinline__ void shift_in(cf2 (&win)[R], cf2 v) {
 #pragma unroll
     for (int r = R - 1; r > 0; --r) win[r] = win[r - 1];
     win[0] = v;
@@ -225,56 +263,93 @@ __device__ __forceinline__ void shift_in(float2 (&win)[R], float2 v) {
 template <int SPS, int OUT_MODE, typename OutT>
 __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
     using C = TxCfg<SPS>;
-    constexpr int R = C::R, NT = C::NT, TS = C::TS, CH = C::CH;
+    constexpr int R = C::R, NT = C::NT, TS = C::TS, CH = C::CH, U = C::U;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int tid = threadIdx.x;
     const int K = p.K;
+    const int NE = TS + K - 1;                         // symbols staged per tile
+    float2* lut_s = lds + ((TS + K + 2) & ~1);         // LUT after the symbol window
     if (blockIdx.x == 0) tx_state_update(p);
-    const int64_t m0 = (int64_t)blockIdx.x * TS;
-    if (m0 >= p.nsym) return;   // workgroup-uniform
+    for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = p.lut[i];
 
-    // 1. symbols m0-(K-1) .. m0+TS-1 -> lds[1 ..]; lds[0] is a pad for the last shift-in.
-    for (int e = tid; e < TS + K - 1; e += NT) lds[1 + e] = tx_symbol_value(p, m0 - (K - 1) + e);
-    __syncthreads();
+    // Persistent workgroup: a balanced contiguous range of tiles.
+    const int64_t ntiles = (p.nsym + TS - 1) / TS;
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    const bool pf = p.fast_bits && p.nsym_valid > 0;   // workgroup-uniform
+    uint64_t pre[U];
+    if (pf) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre[u] = tx_load_word(p, t0 * TS - (K - 1) + tid + NT * u);
+    }
+    __syncthreads();   // LUT visible
 
-    // 2. polyphase FIR, R symbols x SPS phases per lane.
-    float ar[R][SPS], ai[R][SPS];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int q = 0; q < SPS; ++q) { ar[r][q] = 0.f; ai[r][q] = 0.f; }
-    const float2* base = lds + 1 + tid * R + (K - 1);   // base[j] = a[m0 + tid*R + j]
-    float2 win[R];                                      // win[r] = a[m + r - t]
-#pragma unroll
-    for (int r = 0; r < R; ++r) win[r] = base[r];
     cfloat* taps = (cfloat*)p.taps;
-    int t = 0;
-    for (; t + CH <= K; t += CH) {
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t m0 = t * TS;
+        // 1. stage symbols m0-(K-1) .. m0+TS-1 -> lds[1 ..] (lds[0]: pad for the last shift-in)
 #pragma unroll
-        for (int c = 0; c < CH; ++c) {
-            tx_mac<SPS, R>(ar, ai, win, taps + (t + c) * SPS);
-            shift_in<R>(win, base[-(t + c + 1)]);
+        for (int u = 0; u < U; ++u) {
+            const int e = tid + NT * u;
+            if (e < NE) {
+                const int64_t m = m0 - (K - 1) + e;
+                float2 v;
+                if (m < 0) v = p.hist[m + K - 1];
+                else if (m >= p.nsym_valid) v = make_float2(0.f, 0.f);
+                else v = lut_s[pf ? word_index(pre[u], p.bps) : tx_symbol_index(p, m)];
+                lds[1 + e] = v;
+            }
         }
-    }
-    for (; t < K; ++t) {
-        tx_mac<SPS, R>(ar, ai, win, taps + t * SPS);
-        shift_in<R>(win, base[-(t + 1)]);
-    }
-    __syncthreads();
+        for (int e = tid + NT * U; e < NE; e += NT) {   // only for very long filters
+            const int64_t m = m0 - (K - 1) + e;
+            lds[1 + e] = m < 0 ? p.hist[m + K - 1]
+                               : (m >= p.nsym_valid ? make_float2(0.f, 0.f) : lut_s[tx_symbol_index(p, m)]);
+        }
+        __syncthreads();
+        if (pf && t + 1 < t1) {                          // next tile's bits fly during the FIR
+#pragma unroll
+            for (int u = 0; u < U; ++u) pre[u] = tx_load_word(p, m0 + TS - (K - 1) + tid + NT * u);
+        }
 
-    // 3. tile transpose: lane-blocked samples -> LDS -> consecutive pairs per lane.
+        // 2. polyphase FIR, R symbols x SPS phases per lane.
+        cf2 acc[R][SPS];
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int q = 0; q < SPS; ++q)
-            lds[(tid * R + r) * SPS + q] = make_float2(ar[r][q], ai[r][q]);
-    __syncthreads();
-    const int64_t nsym_here = p.nsym - m0 < TS ? p.nsym - m0 : TS;
-    const int nsamp = (int)nsym_here * SPS;
-    const int64_t j0 = m0 * SPS;
-    for (int i = 2 * tid; i < nsamp; i += 2 * NT) {
-        const bool two = i + 1 < nsamp;
-        tx_emit<OUT_MODE, OutT>(p, j0 + i, lds[i], two ? lds[i + 1] : make_float2(0.f, 0.f), two);
+            for (int q = 0; q < SPS; ++q) acc[r][q] = (cf2){0.f, 0.f};
+        const float2* base = lds + 1 + tid * R + (K - 1);   // base[j] = a[m0 + tid*R + j]
+        cf2 win[R];                                         // win[r] = a[m + r - t]
+#pragma unroll
+        for (int r = 0; r < R; ++r) win[r] = ldc(base + r);
+        int k = 0;
+        for (; k + CH <= K; k += CH) {
+            const float2* pc = base - (k + CH);   // positive ds_read immediates: pc[CH-1-c]
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                tx_mac<SPS, R>(acc, win, taps + (k + c) * SPS);
+                shift_in<R>(win, ldc(pc + CH - 1 - c));
+            }
+        }
+        for (; k < K; ++k) {
+            tx_mac<SPS, R>(acc, win, taps + k * SPS);
+            shift_in<R>(win, ldc(base - (k + 1)));
+        }
+
+        // 3. carrier mix + store straight from registers: R*SPS consecutive samples.
+        const int64_t j0 = (m0 + tid * R) * SPS;
+        const int64_t jend = p.nsym * SPS;
+#pragma unroll
+        for (int i = 0; i < R * SPS; i += 2) {
+            const int64_t j = j0 + i;
+            if (j < jend) {
+                const bool two = (i + 1 < R * SPS) && (j + 1 < jend);
+                const cf2 a0 = acc[i / SPS][i % SPS];
+                const int i1 = i + 1 < R * SPS ? i + 1 : i;
+                const cf2 a1 = acc[i1 / SPS][i1 % SPS];
+                const float2 y0 = make_float2(a0.x, a0.y), y1 = make_float2(a1.x, a1.y);
+                tx_emit<OUT_MODE, OutT>(p, j, y0, y1, two);
+            }
+        }
+        __syncthreads();   // the window is restaged next trip
     }
 }
 
@@ -307,6 +382,14 @@ __global__ __launch_bounds__(256) void tx_generic(const TxParams p) {
 // -------------------------------------------------------------------------------- RX ----
 template <typename InT> struct InIO;
 template <> struct InIO<float> {
+    using Raw = float4;   // two consecutive samples
+    __device__ static Raw load_raw(const void* x, int64_t q) {
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(x) + q);
+    }
+    __device__ static void split(Raw v, float2& a, float2& b) {
+        a = make_float2(v.x, v.y);
+        b = make_float2(v.z, v.w);
+    }
     __device__ static float2 load(const void* x, int64_t q) {
         return reinterpret_cast<const float2*>(x)[q];
     }
@@ -320,6 +403,14 @@ template <> struct InIO<float> {
     }
 };
 template <> struct InIO<__half> {
+    using Raw = uint2;
+    __device__ static Raw load_raw(const void* x, int64_t q) {
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const __half2*>(x) + q);
+    }
+    __device__ static void split(Raw u, float2& a, float2& b) {
+        a = __half22float2(*reinterpret_cast<const __half2*>(&u.x));
+        b = __half22float2(*reinterpret_cast<const __half2*>(&u.y));
+    }
     __device__ static float2 load(const void* x, int64_t q) {
         return __half22float2(reinterpret_cast<const __half2*>(x)[q]);
     }
@@ -339,6 +430,7 @@ enum { SLICER_NONE = 0, SLICER_NEAREST = 1, SLICER_QAM_AXIS = 2 };
 // Sample q of the chunk (q < 0: history; q >= N: past the chunk, zero).
 template <typename InT>
 __device__ __forceinline__ float2 rx_sample(const RxParams& p, int64_t q) {
+    if (q < -(int64_t)p.HL) return make_float2(0.f, 0.f);
     if (q >= 0) return q < p.N ? InIO<InT>::load(p.x, q) : make_float2(0.f, 0.f);
     return InIO<InT>::load(p.hist, q + p.HL);
 }
@@ -353,12 +445,13 @@ __device__ __forceinline__ void rx_pair(const RxParams& p, int64_t q, float2& a,
     }
 }
 
-// x * e^{-j phase} (or the reference's x.re * (cos, -sin), demodulator.rs:46,53-54).
+// x * e^{-j phase} (or the reference's x.re * (cos, -sin), demodulator.rs:46,53-54) for
+// stream index n = nb + off (nb wave-uniform).
 template <int MIX>
-__device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t n, float2 x) {
-    if (n < 0) return make_float2(0.f, 0.f);   // before the stream: zero history
+__device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t nb, int off, float2 x) {
+    if (nb + off < 0) return make_float2(0.f, 0.f);   // before the stream: zero history
     float s, c;
-    sincos_phase(carrier_phase(p.w, p.c0 + (uint64_t)n, p.small_n), s, c);
+    sincos_phase(carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.small_n), s, c);
     if (MIX == MIX_REFERENCE_REAL) return make_float2(x.x * c, x.x * -s);
     return make_float2(__builtin_fmaf(x.y, s, x.x * c), __builtin_fmaf(-x.x, s, x.y * c));
 }
@@ -402,90 +495,158 @@ __device__ void rx_state_update(const RxParams& p) {
 }
 
 template <int DEC> struct RxCfg {
-    static constexpr int R = DEC == 1 ? 9 : DEC == 2 ? 7 : DEC == 4 ? 5 : DEC == 8 ? 3 : 1;
+    static constexpr int R = DEC == 1 ? 9 : DEC == 2 ? 7 : DEC == 4 ? 5 : DEC == 8 ? 3 : 1;  // odd
     static constexpr int NT = 256;
-    static constexpr int TS = NT * R;   // output symbols per workgroup
+    static constexpr int TS = NT * R;   // output symbols per tile
     static constexpr int CH = 8;
+    // taps per branch the prefetch ring covers (longer filters take the slow staging path)
+    static constexpr int KMAX = DEC == 1 ? 65 : DEC == 8 ? 65 : 33;
+    // sample pairs prefetched per lane: covers (TS + KMAX - 1) * DEC samples
+    static constexpr int U = ((TS + KMAX - 1) * DEC + 2 * NT - 1) / (2 * NT);
 };
 
 template <int R>
-__device__ __forceinline__ void rx_mac(float (&ar)[R], float (&ai)[R], const float2 (&win)[R],
-                                       float h) {
+__device__ __forceinline__ void rx_mac(cf2 (&acc)[R], const cf2 (&win)[R], float h) {
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-        ar[i] = __builtin_fmaf(win[i].x, h, ar[i]);
-        ai[i] = __builtin_fmaf(win[i].y, h, ai[i]);
-    }
+    for (int i = 0; i < R; ++i) acc[i] = cmac(win[i], h, acc[i]);
 }
 
 // Plane stride (float2 elements): TS + K rounded to an odd count (bank spread of the
 // per-plane base); lanes read with stride R (odd) -> conflict-free ds_read_b64.
 __host__ __device__ inline int rx_plane_stride(int TS, int K) { return (TS + K) | 1; }
 
+// Rare path (first / last tile of a chunk, unaligned input, carrier index >= 2^32): one
+// sample at a time with full 64-bit bookkeeping; kept out of line so its index arithmetic
+// does not occupy registers in the steady-state loop.
+template <int DEC, typename InT, int MIX>
+__device__ __noinline__ void rx_stage_slow(const RxParams& p, float2* lds, int PS, int NS,
+                                           int64_t q_lo) {
+    const int64_t n_lo = q_lo + p.n_start;
+    for (int e = threadIdx.x; e < NS; e += blockDim.x) {
+        const float2 z = rx_mix<MIX>(p, n_lo, e, rx_sample<InT>(p, q_lo + e));
+        const int em = e / DEC, b = DEC - 1 - (e - em * DEC);   // z_b[m] = z[m*DEC + D - b]
+        lds[b * PS + 1 + em] = z;
+    }
+}
+
+// Steady state: every staged sample lies inside the chunk and below carrier index 2^32.
+// Slot u of lane tid holds samples e = 2*(tid + NT*u) - PAR + {0,1}; the per-slot part of
+// every index is a compile-time constant (NT*2/DEC plane elements per slot), so the LDS
+// stores use immediate offsets and the phase needs one 32-bit add.
+template <int DEC, typename InT, int MIX, int PAR, int U, int NT>
+__device__ __forceinline__ void rx_stage_fast(const RxParams& p, float2* lds, int PS, int NS,
+                                              uint32_t nb32, const typename InIO<InT>::Raw (&pre)[U]) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        float2 x[2];
+        InIO<InT>::split(pre[u], x[0], x[1]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int el = 2 * tid - PAR + j;           // lane part of e (>= -1)
+            const int e = el + 2 * NT * u;
+            if (e >= 0 && e < NS) {
+                float s, c;
+                sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)e)), s, c);
+                float2 z;
+                if (MIX == MIX_REFERENCE_REAL) z = make_float2(x[j].x * c, x[j].x * -s);
+                else z = make_float2(__builtin_fmaf(x[j].y, s, x[j].x * c),
+                                     __builtin_fmaf(-x[j].x, s, x[j].y * c));
+                const int em_l = (el + DEC) / DEC - 1;  // floor(el / DEC), el >= -1
+                const int b = DEC - 1 - (el + DEC - (em_l + 1) * DEC);
+                lds[b * PS + 1 + em_l + (2 * NT / DEC) * u] = z;
+            }
+        }
+    }
+}
+
 template <int DEC, typename InT, int MIX, typename OutT>
 __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
     using C = RxCfg<DEC>;
-    constexpr int R = C::R, NT = C::NT, TS = C::TS, CH = C::CH;
+    using IO = InIO<InT>;
+    using Raw = typename IO::Raw;
+    constexpr int R = C::R, NT = C::NT, TS = C::TS, CH = C::CH, U = C::U;
+    static_assert((2 * NT) % DEC == 0, "slot stride must be whole plane elements");
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int tid = threadIdx.x;
     const int K = p.K;
     const int PS = rx_plane_stride(TS, K);
+    const int NS = (TS + K - 1) * DEC;             // samples staged per tile
     if (blockIdx.x == 0) rx_state_update<InT>(p);
-    const int64_t k0 = p.k_first + (int64_t)blockIdx.x * TS;
-    if ((int64_t)blockIdx.x * TS >= p.nout) return;   // workgroup-uniform
 
-    // 1. samples n_lo .. n_lo + NS - 1 (stream indices), mixed, into planes:
-    //    sample e -> plane b = DEC-1 - e%DEC, index e/DEC   (z_b[m] = z[m*DEC + D - b]).
-    const int64_t n_lo = k0 * DEC + p.D - (int64_t)K * DEC + 1;
-    const int64_t q_lo = n_lo - p.n_start;
-    const int NS = (TS + K - 1) * DEC;
-    const int par = (int)(q_lo & 1);
-    for (int e = 2 * tid - par; e < NS; e += 2 * NT) {
-        float2 x0, x1;
-        rx_pair<InT>(p, q_lo + e, x0, x1);
+    // Persistent workgroup: a balanced contiguous range of tiles of kept instants.
+    const int64_t ntiles = (p.nout + TS - 1) / TS;
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    // tile t stages stream samples n_lo(t) .. n_lo(t) + NS - 1; chunk index q = n - n_start
+    auto q_lo_of = [&](int64_t t) {
+        return (p.k_first + t * TS) * DEC + p.D - (int64_t)K * DEC + 1 - p.n_start;
+    };
+    // A tile is "inside" when its prefetched slots are whole pairs of this chunk.
+    const bool pf = p.x_aligned16 && p.small_n && NS <= 2 * NT * U;   // workgroup-uniform
+    auto inside = [&](int64_t q_lo) {
+        const int64_t qb = q_lo - (q_lo & 1);
+        return pf && qb >= 0 && qb + 2 * NT * U <= p.N;
+    };
+    Raw pre[U];
+    auto prefetch = [&](int64_t q_lo) {
+        const Raw* xb = reinterpret_cast<const Raw*>(p.x) + ((q_lo - (q_lo & 1)) >> 1);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int eu = e + u;
-            if (eu < 0 || eu >= NS) continue;
-            const float2 z = rx_mix<MIX>(p, n_lo + eu, u ? x1 : x0);
-            const int em = eu / DEC, b = DEC - 1 - (eu - em * DEC);
-            lds[b * PS + 1 + em] = z;
-        }
-    }
-    __syncthreads();
+        for (int u = 0; u < U; ++u) pre[u] = xb[tid + NT * u];
+    };
+    if (t0 < t1 && inside(q_lo_of(t0))) prefetch(q_lo_of(t0));
 
-    // 2. matched filter at the kept instants, R consecutive outputs per lane.
-    float ar[R], ai[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) { ar[i] = 0.f; ai[i] = 0.f; }
     cfloat* taps = (cfloat*)p.taps;
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t q_lo = q_lo_of(t);
+        // 1. mix the tile's samples into DEC polyphase planes.
+        if (inside(q_lo)) {
+            const uint32_t nb32 = (uint32_t)(p.c0 + (uint64_t)(q_lo - (q_lo & 1) + p.n_start));
+            if (q_lo & 1) rx_stage_fast<DEC, InT, MIX, 1, U, NT>(p, lds, PS, NS, nb32 + 1u, pre);
+            else rx_stage_fast<DEC, InT, MIX, 0, U, NT>(p, lds, PS, NS, nb32, pre);
+        } else {
+            rx_stage_slow<DEC, InT, MIX>(p, lds, PS, NS, q_lo);
+        }
+        __syncthreads();
+        if (t + 1 < t1) {                       // next tile's samples fly during the filter
+            const int64_t qn = q_lo_of(t + 1);
+            if (inside(qn)) prefetch(qn);
+        }
+
+
+        // 2. matched filter at the kept instants, R consecutive outputs per lane.
+        cf2 acc[R];
 #pragma unroll
-    for (int b = 0; b < DEC; ++b) {
-        const float2* base = lds + b * PS + 1 + tid * R + (K - 1);   // base[j] = z_b[k+j]
-        cfloat* hb = taps + b * K;
-        float2 win[R];
+        for (int i = 0; i < R; ++i) acc[i] = (cf2){0.f, 0.f};
+#pragma unroll 1
+        for (int b = 0; b < DEC; ++b) {
+            const float2* base = lds + b * PS + 1 + tid * R + (K - 1);   // base[j] = z_b[k+j]
+            cfloat* hb = taps + b * K;
+            cf2 win[R];
 #pragma unroll
-        for (int i = 0; i < R; ++i) win[i] = base[i];
-        int t = 0;
-        for (; t + CH <= K; t += CH) {
+            for (int i = 0; i < R; ++i) win[i] = ldc(base + i);
+            int k = 0;
+            for (; k + CH <= K; k += CH) {
+                const float2* pc = base - (k + CH);   // positive ds_read immediates
 #pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                rx_mac<R>(ar, ai, win, hb[t + c]);
-                shift_in<R>(win, base[-(t + c + 1)]);
+                for (int c = 0; c < CH; ++c) {
+                    rx_mac<R>(acc, win, hb[k + c]);
+                    shift_in<R>(win, ldc(pc + CH - 1 - c));
+                }
+            }
+            for (; k < K; ++k) {
+                rx_mac<R>(acc, win, hb[k]);
+                shift_in<R>(win, ldc(base - (k + 1)));
             }
         }
-        for (; t < K; ++t) {
-            rx_mac<R>(ar, ai, win, hb[t]);
-            shift_in<R>(win, base[-(t + 1)]);
-        }
-    }
 
-    // 3. decisions + stores.
-    const float g = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
+        // 3. decisions + stores.
+        const float g = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-        const int64_t o = (int64_t)blockIdx.x * TS + tid * R + i;
-        if (o < p.nout) rx_emit<OutT>(p, o, g * ar[i], g * ai[i]);
+        for (int i = 0; i < R; ++i) {
+            const int64_t o = t * TS + tid * R + i;
+            if (o < p.nout) rx_emit<OutT>(p, o, g * acc[i].x, g * acc[i].y);
+        }
+        __syncthreads();   // planes are restaged next trip
     }
 }
 
@@ -501,7 +662,7 @@ __global__ __launch_bounds__(64) void rx_generic(const RxParams p) {
     const int64_t n_lo = k0 * DEC + p.D - (L - 1);
     const int NS = (TS - 1) * DEC + L;
     for (int e = threadIdx.x; e < NS; e += TS)
-        lds[e] = rx_mix<MIX>(p, n_lo + e, rx_sample<InT>(p, n_lo + e - p.n_start));
+        lds[e] = rx_mix<MIX>(p, n_lo, e, rx_sample<InT>(p, n_lo + e - p.n_start));
     __syncthreads();
     const int64_t o = (int64_t)blockIdx.x * TS + threadIdx.x;
     if (o >= p.nout) return;
@@ -614,14 +775,50 @@ __global__ __launch_bounds__(256) void prng_bits(uint64_t seed, uint8_t* out, si
 }
 
 // ---------------------------------------------------------------------- dispatch ----
+// Persistent grids: resident workgroups per CU (occupancy API, cached per kernel and LDS
+// size) x CUs, never more than the number of tiles.
+static int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
+static std::mutex g_occ_mu;
+static std::map<std::pair<const void*, size_t>, int> g_occ;
+
+static int resident_blocks(const void* kernel, int threads, size_t lds) {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto key = std::make_pair(kernel, lds);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) return it->second;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, threads, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    g_occ[key] = occ;
+    return occ;
+}
+
+static unsigned persistent_grid(const void* kernel, int threads, size_t lds, int64_t ntiles) {
+    const int64_t cap = (int64_t)resident_blocks(kernel, threads, lds) * device_cus();
+    const int64_t g = ntiles < cap ? ntiles : cap;
+    return (unsigned)(g > 0 ? g : 1);
+}
+
 template <int SPS, int OM, typename OutT>
 static hipError_t tx_go(const TxParams& p, hipStream_t s) {
     using C = TxCfg<SPS>;
-    const int64_t nblk = (p.nsym + C::TS - 1) / C::TS;
-    const size_t a = (size_t)(C::TS + p.K) * sizeof(float2);
-    const size_t b = (size_t)C::TS * SPS * sizeof(float2);
-    const size_t lds = a > b ? a : b;
-    hipLaunchKernelGGL((tx_fast<SPS, OM, OutT>), dim3((unsigned)(nblk > 0 ? nblk : 1)),
+    const int64_t ntiles = (p.nsym + C::TS - 1) / C::TS;
+    const size_t lds = ((size_t)((C::TS + p.K + 2) & ~1) + ((size_t)1 << p.bps)) * sizeof(float2);
+    const void* k = reinterpret_cast<const void*>(&tx_fast<SPS, OM, OutT>);
+    hipLaunchKernelGGL((tx_fast<SPS, OM, OutT>), dim3(persistent_grid(k, C::NT, lds, ntiles)),
                        dim3(C::NT), lds, s, p);
     return hipGetLastError();
 }
@@ -660,9 +857,10 @@ hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStr
 template <int DEC, typename InT, int MIX, typename OutT>
 static hipError_t rx_go(const RxParams& p, hipStream_t s) {
     using C = RxCfg<DEC>;
-    const int64_t nblk = (p.nout + C::TS - 1) / C::TS;
+    const int64_t ntiles = (p.nout + C::TS - 1) / C::TS;
     const size_t lds = ((size_t)DEC * rx_plane_stride(C::TS, p.K) + 1) * sizeof(float2);
-    hipLaunchKernelGGL((rx_fast<DEC, InT, MIX, OutT>), dim3((unsigned)(nblk > 0 ? nblk : 1)),
+    const void* k = reinterpret_cast<const void*>(&rx_fast<DEC, InT, MIX, OutT>);
+    hipLaunchKernelGGL((rx_fast<DEC, InT, MIX, OutT>), dim3(persistent_grid(k, C::NT, lds, ntiles)),
                        dim3(C::NT), lds, s, p);
     return hipGetLastError();
 }
