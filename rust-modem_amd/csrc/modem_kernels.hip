@@ -209,6 +209,31 @@ __device__ __forceinline__ void tx_emit(const TxParams& p, int64_t j, float2 y0,
     }
 }
 
+// Same with the sample index split into a wave-uniform base and a 32-bit lane offset.
+template <int OUT_MODE, typename OutT>
+__device__ __forceinline__ void tx_emit_off(const TxParams& p, int64_t jb, int off, float2 y0, float2 y1,
+                                            bool two) {
+    const int64_t j = jb + off;
+    float2 z0 = y0, z1 = y1;
+    if (OUT_MODE != OUT_IQ_BASEBAND) {
+        const uint64_t nb = p.s0 + (uint64_t)jb;
+        float s, c;
+        sincos_phase(carrier_phase_off(p.w, nb, off, p.small_n), s, c);
+        z0 = make_float2(y0.x * c - y0.y * s, y0.x * s + y0.y * c);
+        if (two) {
+            sincos_phase(carrier_phase_off(p.w, nb, off + 1, p.small_n), s, c);
+            z1 = make_float2(y1.x * c - y1.y * s, y1.x * s + y1.y * c);
+        }
+    }
+    if (two) {
+        if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_pair(p.out, j, z0.x, z1.x);
+        else OutIO<OutT>::store_pair(p.out, j, z0.x, z0.y, z1.x, z1.y);
+    } else {
+        if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, j, z0.x);
+        else OutIO<OutT>::store_one(p.out, j, z0.x, z0.y);
+    }
+}
+
 template <int SPS> struct TxCfg {
     // R consecutive symbols per lane -> R*SPS consecutive output samples per lane
     // (R*SPS*8 B, so a store instruction touches 64-B pieces of 16-32 lines).
@@ -219,13 +244,11 @@ template <int SPS> struct TxCfg {
     static constexpr int U = (TS + NT) / NT;     // staging slots prefetched per lane
 };
 
-// Raw bits word of symbol m (fast path: one aligned 1/2/4/8-byte load). The address is
-// clamped so the load is unconditional (no per-element branch around it); symbols outside
-// [0, nsym_valid) are fixed up when staged.
-__device__ __forceinline__ uint64_t tx_load_word(const TxParams& p, int64_t m) {
-    const int64_t mc = m < 0 ? 0 : (m >= p.nsym_valid ? p.nsym_valid - 1 : m);
-    const uint8_t* b = p.bits + mc * p.bps;
-    switch (p.bps) {
+// Raw bits word of symbol m (fast path: one aligned 1/2/4/8-byte load; the caller only asks
+// for symbols of this call, so the load is unconditional).
+__device__ __forceinline__ uint64_t tx_load_word(const uint8_t* bits, int bps, int64_t m) {
+    const uint8_t* b = bits + m * bps;
+    switch (bps) {
     case 1: return *b;
     case 2: return *reinterpret_cast<const uint16_t*>(b);
     case 4: return *reinterpret_cast<const uint32_t*>(b);
@@ -233,13 +256,16 @@ __device__ __forceinline__ uint64_t tx_load_word(const TxParams& p, int64_t m) {
     }
 }
 
-// bytes_to_bits (digital/util.rs:5-11) of a little-endian word holding bps bytes.
+// bytes_to_bits (digital/util.rs:5-11) of a little-endian word holding bps bytes, branch-free:
+// the LSB of byte i sits at bit 8i; one multiply moves it to bit 27-i (32-bit form) or 63-i
+// (64-bit form) without carries (all partial-product bit positions are distinct).
 __device__ __forceinline__ uint32_t word_index(uint64_t v, int bps) {
-    uint32_t idx = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-        if (q < bps) idx |= (uint32_t)((v >> (8 * q)) & 1u) << (bps - 1 - q);
-    return idx;
+    if (bps <= 4) {
+        const uint32_t b = (uint32_t)v & 0x01010101u;
+        return ((b * 0x08040201u) >> 24) >> (4 - bps);
+    }
+    const uint64_t b = v & 0x0101010101010101ull;
+    return (uint32_t)((b * 0x8040201008040201ull) >> 56) >> (8 - bps);
 }
 
 template <int SPS, int R>
@@ -275,40 +301,41 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
     // Persistent workgroup: a balanced contiguous range of tiles.
     const int64_t ntiles = (p.nsym + TS - 1) / TS;
     const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
-    const bool pf = p.fast_bits && p.nsym_valid > 0;   // workgroup-uniform
+    // "inside": every staged symbol is a data symbol of this call and the prefetch ring
+    // covers the window -> unconditional loads, no per-element cases.
+    const bool pf = p.fast_bits && NE <= NT * U;        // workgroup-uniform
+    auto inside = [&](int64_t m0) { return pf && m0 - (K - 1) >= 0 && m0 + TS <= p.nsym_valid; };
     uint64_t pre[U];
-    if (pf) {
+    auto prefetch = [&](int64_t m0) {
+        const int64_t mb = m0 - (K - 1);
 #pragma unroll
-        for (int u = 0; u < U; ++u) pre[u] = tx_load_word(p, t0 * TS - (K - 1) + tid + NT * u);
-    }
+        for (int u = 0; u < U; ++u) {
+            const int e = tid + NT * u;
+            pre[u] = tx_load_word(p.bits, p.bps, mb + (e < NE ? e : NE - 1));
+        }
+    };
+    if (t0 < t1 && inside(t0 * TS)) prefetch(t0 * TS);
     __syncthreads();   // LUT visible
 
     cfloat* taps = (cfloat*)p.taps;
     for (int64_t t = t0; t < t1; ++t) {
         const int64_t m0 = t * TS;
         // 1. stage symbols m0-(K-1) .. m0+TS-1 -> lds[1 ..] (lds[0]: pad for the last shift-in)
+        if (inside(m0)) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = tid + NT * u;
-            if (e < NE) {
+            for (int u = 0; u < U; ++u) {
+                const int e = tid + NT * u;
+                if (e < NE) lds[1 + e] = lut_s[word_index(pre[u], p.bps)];
+            }
+        } else {   // first / last tiles, leftover bits, flush: one symbol at a time
+            for (int e = tid; e < NE; e += NT) {
                 const int64_t m = m0 - (K - 1) + e;
-                float2 v;
-                if (m < 0) v = p.hist[m + K - 1];
-                else if (m >= p.nsym_valid) v = make_float2(0.f, 0.f);
-                else v = lut_s[pf ? word_index(pre[u], p.bps) : tx_symbol_index(p, m)];
-                lds[1 + e] = v;
+                lds[1 + e] = m < 0 ? p.hist[m + K - 1]
+                                   : (m >= p.nsym_valid ? make_float2(0.f, 0.f) : lut_s[tx_symbol_index(p, m)]);
             }
         }
-        for (int e = tid + NT * U; e < NE; e += NT) {   // only for very long filters
-            const int64_t m = m0 - (K - 1) + e;
-            lds[1 + e] = m < 0 ? p.hist[m + K - 1]
-                               : (m >= p.nsym_valid ? make_float2(0.f, 0.f) : lut_s[tx_symbol_index(p, m)]);
-        }
         __syncthreads();
-        if (pf && t + 1 < t1) {                          // next tile's bits fly during the FIR
-#pragma unroll
-            for (int u = 0; u < U; ++u) pre[u] = tx_load_word(p, m0 + TS - (K - 1) + tid + NT * u);
-        }
+        if (t + 1 < t1 && inside(m0 + TS)) prefetch(m0 + TS);   // next bits fly during the FIR
 
         // 2. polyphase FIR, R symbols x SPS phases per lane.
         cf2 acc[R][SPS];
@@ -335,18 +362,18 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
         }
 
         // 3. carrier mix + store straight from registers: R*SPS consecutive samples.
-        const int64_t j0 = (m0 + tid * R) * SPS;
+        const int64_t jt = m0 * SPS;                 // first sample of the tile (uniform)
+        const int jl = tid * R * SPS;                // lane offset within the tile
         const int64_t jend = p.nsym * SPS;
 #pragma unroll
         for (int i = 0; i < R * SPS; i += 2) {
-            const int64_t j = j0 + i;
+            const int64_t j = jt + jl + i;
             if (j < jend) {
                 const bool two = (i + 1 < R * SPS) && (j + 1 < jend);
                 const cf2 a0 = acc[i / SPS][i % SPS];
                 const int i1 = i + 1 < R * SPS ? i + 1 : i;
                 const cf2 a1 = acc[i1 / SPS][i1 % SPS];
-                const float2 y0 = make_float2(a0.x, a0.y), y1 = make_float2(a1.x, a1.y);
-                tx_emit<OUT_MODE, OutT>(p, j, y0, y1, two);
+                tx_emit_off<OUT_MODE, OutT>(p, jt, jl + i, make_float2(a0.x, a0.y), make_float2(a1.x, a1.y), two);
             }
         }
         __syncthreads();   // the window is restaged next trip
@@ -501,8 +528,9 @@ template <int DEC> struct RxCfg {
     static constexpr int CH = 8;
     // taps per branch the prefetch ring covers (longer filters take the slow staging path)
     static constexpr int KMAX = DEC == 1 ? 65 : DEC == 8 ? 65 : 33;
-    // sample pairs prefetched per lane: covers (TS + KMAX - 1) * DEC samples
-    static constexpr int U = ((TS + KMAX - 1) * DEC + 2 * NT - 1) / (2 * NT);
+    // sample pairs prefetched per lane: covers (TS + KMAX - 1) * DEC samples plus one
+    // (a tile whose first sample is odd starts its pairs one sample early)
+    static constexpr int U = ((TS + KMAX - 1) * DEC + 1 + 2 * NT - 1) / (2 * NT);
 };
 
 template <int R>
@@ -516,10 +544,10 @@ __device__ __forceinline__ void rx_mac(cf2 (&acc)[R], const cf2 (&win)[R], float
 __host__ __device__ inline int rx_plane_stride(int TS, int K) { return (TS + K) | 1; }
 
 // Rare path (first / last tile of a chunk, unaligned input, carrier index >= 2^32): one
-// sample at a time with full 64-bit bookkeeping; kept out of line so its index arithmetic
-// does not occupy registers in the steady-state loop.
+// sample at a time with full 64-bit bookkeeping, as one rolled loop under a uniform branch
+// (never called out of line: a call would push the kernel arguments to per-lane scratch).
 template <int DEC, typename InT, int MIX>
-__device__ __noinline__ void rx_stage_slow(const RxParams& p, float2* lds, int PS, int NS,
+__device__ __forceinline__ void rx_stage_slow(const RxParams& p, float2* lds, int PS, int NS,
                                            int64_t q_lo) {
     const int64_t n_lo = q_lo + p.n_start;
     for (int e = threadIdx.x; e < NS; e += blockDim.x) {
@@ -582,7 +610,7 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
         return (p.k_first + t * TS) * DEC + p.D - (int64_t)K * DEC + 1 - p.n_start;
     };
     // A tile is "inside" when its prefetched slots are whole pairs of this chunk.
-    const bool pf = p.x_aligned16 && p.small_n && NS <= 2 * NT * U;   // workgroup-uniform
+    const bool pf = p.x_aligned16 && p.small_n && NS + 1 <= 2 * NT * U;   // workgroup-uniform
     auto inside = [&](int64_t q_lo) {
         const int64_t qb = q_lo - (q_lo & 1);
         return pf && qb >= 0 && qb + 2 * NT * U <= p.N;

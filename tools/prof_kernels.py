@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Profiling driver: run the TX and RX kernels of one bench workload `--reps` times
+(device-resident buffers, no oracle). Used under rocprofv3 for traces and PMC counters."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=sorted(bench.WORKLOADS))
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--only", choices=["tx", "rx", "both"], default="both")
+    a = ap.parse_args()
+    r = bench.GpuRunner(bench.WORKLOADS[a.config], 0, 0)
+    for _ in range(a.reps):
+        for c in range(r.nch):
+            if a.only in ("tx", "both"):
+                r.tx(c)
+            if a.only in ("rx", "both"):
+                r.rx(c)
+    r.sync()
+    print("ok", r.check())
+
+
+if __name__ == "__main__":
+    main()
