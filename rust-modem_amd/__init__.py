@@ -66,7 +66,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def lib_path() -> str:
-    return os.path.join(_HERE, "lib", "libmodem_hip.so")
+    # RUST_MODEM_AMD_LIB: an alternative build (profiling ablations, tools/ablate.sh)
+    return os.environ.get("RUST_MODEM_AMD_LIB") or os.path.join(_HERE, "lib", "libmodem_hip.so")
 
 
 class _Ring(ctypes.Structure):

@@ -292,11 +292,13 @@ struct modem_tx {
     float2* d_hist[2] = {nullptr, nullptr};
     uint8_t* d_carry[2] = {nullptr, nullptr};
     int hcur = 0, ccur = 0, ncarry = 0;
+    int mfma_ksteps = 0;            // > 0: FIR on the matrix pipe (tx_mfma)
+    float* d_bfrag = nullptr;       // its per-lane B fragments [ksteps][64]
     Stage bits_stage, out_stage;
     ~modem_tx() {
         DeviceGuard g(device);
         for (void* p : {(void*)d_lut, (void*)d_taps, (void*)d_hist[0], (void*)d_hist[1],
-                        (void*)d_carry[0], (void*)d_carry[1]})
+                        (void*)d_carry[0], (void*)d_carry[1], (void*)d_bfrag})
             if (p) (void)hipFree(p);
     }
 };
@@ -330,7 +332,9 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     // ntaps == 0: the reference's sample-and-hold == zero-stuffing + sps unit taps.
     const uint32_t L = d->ntaps ? d->ntaps : d->samples_per_symbol;
     h->K = (L + h->sps - 1) / h->sps;
-    std::vector<float> pp((size_t)h->K * h->sps, 0.0f);   // pp[t*sps + p] = h[p + sps*t]
+    // pp[t*sps + p] = h[p + sps*t]; padded by mk::kTapPad steps of zeros so the kernels'
+    // look-ahead tap loads stay in bounds.
+    std::vector<float> pp((size_t)(h->K + mk::kTapPad) * h->sps, 0.0f);
     for (uint32_t j = 0; j < L; ++j) pp[(size_t)(j / h->sps) * h->sps + j % h->sps] = d->ntaps ? d->taps[j] : 1.0f;
     modem_status st;
     const size_t nl = (size_t)1 << h->bps;
@@ -345,6 +349,29 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
         (void)hipGetLastError();
         delete h;
         return MODEM_ERR_HIP;
+    }
+    // FIR path: the matrix pipe when the (sps, K) shape has an instantiated kernel, unless
+    // MODEM_HIP_FIR=valu forces the packed-VALU kernel (both are parity-tested).
+    const char* env = std::getenv("MODEM_HIP_FIR");
+    const bool force_valu = env && std::strcmp(env, "valu") == 0;
+    h->mfma_ksteps = force_valu ? 0 : mk::tx_mfma_ksteps((int)h->sps, (int)h->K);
+    if (h->mfma_ksteps > 0) {
+        // B[o][j] = h[p + sps*(c + PRE - o)], j = sps*c + p, for lane l / k-step s:
+        // o = 4s + (l >> 4), j = l & 15 (tx_mfma in modem_kernels.hip).
+        const int nks = h->mfma_ksteps, sps = (int)h->sps, SB = 16 / sps, PRE = 4 * nks - SB;
+        std::vector<float> bf((size_t)nks * 64, 0.0f);
+        for (int st = 0; st < nks; ++st)
+            for (int l = 0; l < 64; ++l) {
+                const int o = 4 * st + (l >> 4), j = l & 15, c = j / sps, ph = j % sps;
+                const int t = c + PRE - o;
+                if (t >= 0 && t < (int)h->K) bf[(size_t)st * 64 + l] = pp[(size_t)t * sps + ph];
+            }
+        if ((st = dalloc(&h->d_bfrag, bf.size()))) { delete h; return st; }
+        if (hipMemcpy(h->d_bfrag, bf.data(), bf.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipGetLastError();
+            delete h;
+            return MODEM_ERR_HIP;
+        }
     }
     *out = h;
     return MODEM_OK;
@@ -399,7 +426,10 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
                    ((uintptr_t)dbits % h->bps) == 0) ? 1 : 0;
     p.small_n = (h->sample + nsamp) <= (1ull << 32) ? 1 : 0;
     p.w = h->w;
-    HIP_TRY(mk::launch_tx(p, (int)h->sps, h->dtype, h->out_mode, s));
+    if (h->mfma_ksteps > 0)
+        HIP_TRY(mk::launch_tx_mfma(p, (int)h->sps, h->mfma_ksteps, h->d_bfrag, h->dtype, h->out_mode, s));
+    else
+        HIP_TRY(mk::launch_tx(p, (int)h->sps, h->dtype, h->out_mode, s));
     h->hcur ^= 1;
     if (!flush) { h->ccur ^= 1; h->ncarry = ncarry_new; }
     h->sample += nsamp;
@@ -480,7 +510,8 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
     h->c0 = d->s0;
     h->slicer = sl;
     h->slicer.lut = nullptr;
-    std::vector<float> pp((size_t)h->K * h->decim, 0.0f);   // pp[b*K + t] = h[b + decim*t]
+    // pp[b*K + t] = h[b + decim*t], padded for the kernels' look-ahead tap loads
+    std::vector<float> pp((size_t)h->K * h->decim + mk::kTapPad, 0.0f);
     for (uint32_t j = 0; j < d->ntaps; ++j) pp[(size_t)(j % h->decim) * h->K + j / h->decim] = d->taps[j];
     const size_t esz = rx_in_bytes(h);
     modem_status st;

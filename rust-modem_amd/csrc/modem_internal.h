@@ -74,6 +74,11 @@ struct FirParams {
 // Launchers return hipSuccess or the launch error. They pick a specialised kernel for the
 // common samples-per-symbol values and a generic one otherwise.
 hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s);
+// TX FIR on the matrix pipe: ksteps = window k-steps for (sps, K) or 0 when unsupported;
+// bfrag = per-lane B fragments [ksteps][64] (see tx_mfma in modem_kernels.hip).
+int tx_mfma_ksteps(int sps, int K);
+hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const float* bfrag, int dtype,
+                          int out_mode, hipStream_t s);
 hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,
                      hipStream_t s);
 hipError_t launch_fir(const FirParams& p, hipStream_t s);
@@ -82,5 +87,7 @@ hipError_t launch_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, hipStream
 
 // Largest tap count the kernels accept (LDS budget).
 constexpr int kMaxTaps = 4096;
+// Zero steps appended to the polyphase tap buffers (look-ahead loads of the next chunk).
+constexpr int kTapPad = 16;
 
 }  // namespace mk

@@ -69,6 +69,10 @@ __device__ __forceinline__ float carrier_phase_off(float w, uint64_t base, int o
 // polynomial (<= 2 ulp); the default uses the hardware v_sin_f32/v_cos_f32 (input in
 // revolutions). Either way the sample tolerance is set in tests/test_gpu_parity.py.
 __device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
+#if defined(MODEM_ABLATE_TRIG)        // profiling builds only (tools/ablate.sh)
+    s = ph; c = 1.0f;
+    return;
+#endif
 #ifdef MODEM_PRECISE_TRIG
     const float j = __builtin_rintf(ph * 0.63661977236758134f);
     float r = __builtin_fmaf(-j, 1.57079637050628662f, ph);
@@ -132,7 +136,7 @@ __device__ __forceinline__ uint32_t tx_symbol_index(const TxParams& p, int64_t m
 }
 
 __device__ __forceinline__ float2 tx_symbol_value(const TxParams& p, int64_t m) {
-    if (m < 0) return p.hist[m + p.K - 1];
+    if (m < 0) return m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f);
     if (m >= p.nsym_valid) return make_float2(0.f, 0.f);
     return p.lut[tx_symbol_index(p, m)];
 }
@@ -215,7 +219,11 @@ __device__ __forceinline__ void tx_emit_off(const TxParams& p, int64_t jb, int o
                                             bool two) {
     const int64_t j = jb + off;
     float2 z0 = y0, z1 = y1;
+#ifdef MODEM_ABLATE_MIX
+    if (false) {
+#else
     if (OUT_MODE != OUT_IQ_BASEBAND) {
+#endif
         const uint64_t nb = p.s0 + (uint64_t)jb;
         float s, c;
         sincos_phase(carrier_phase_off(p.w, nb, off, p.small_n), s, c);
@@ -235,13 +243,13 @@ __device__ __forceinline__ void tx_emit_off(const TxParams& p, int64_t jb, int o
 }
 
 template <int SPS> struct TxCfg {
-    // R consecutive symbols per lane -> R*SPS consecutive output samples per lane
-    // (R*SPS*8 B, so a store instruction touches 64-B pieces of 16-32 lines).
-    static constexpr int R = SPS == 1 ? 8 : SPS == 2 ? 4 : SPS == 4 ? 2 : 1;
+    // R consecutive symbols per lane (odd: conflict-free ds_read_b64 of the window) ->
+    // R*SPS consecutive output samples per lane.
+    static constexpr int R = SPS == 1 ? 5 : SPS == 2 ? 3 : 1;
     static constexpr int NT = 256;
     static constexpr int TS = NT * R;            // symbols per tile
-    static constexpr int CH = 8;                 // taps unrolled per loop trip
-    static constexpr int U = (TS + NT) / NT;     // staging slots prefetched per lane
+    static constexpr int CH = 8;                 // taps steps unrolled per loop trip
+    static constexpr int U = (TS + 64 + NT - 1) / NT;    // staging slots prefetched per lane
 };
 
 // Raw bits word of symbol m (fast path: one aligned 1/2/4/8-byte load; the caller only asks
@@ -268,8 +276,8 @@ __device__ __forceinline__ uint32_t word_index(uint64_t v, int bps) {
     return (uint32_t)((b * 0x8040201008040201ull) >> 56) >> (8 - bps);
 }
 
-template <int SPS, int R>
-__device__ __forceinline__ void tx_mac(cf2 (&acc)[R][SPS], const cf2 (&win)[R], cfloat* h) {
+template <int SPS, int R, typename TP>
+__device__ __forceinline__ void tx_mac(cf2 (&acc)[R][SPS], const cf2 (&win)[R], TP h) {
     float hv[SPS];
 #pragma unroll
     for (int q = 0; q < SPS; ++q) hv[q] = h[q];
@@ -348,6 +356,10 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
 #pragma unroll
         for (int r = 0; r < R; ++r) win[r] = ldc(base + r);
         int k = 0;
+#ifdef MODEM_ABLATE_FIR
+        k = K;
+        acc[0][0] = win[0];
+#endif
         for (; k + CH <= K; k += CH) {
             const float2* pc = base - (k + CH);   // positive ds_read immediates: pc[CH-1-c]
 #pragma unroll
@@ -374,6 +386,104 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
                 const int i1 = i + 1 < R * SPS ? i + 1 : i;
                 const cf2 a1 = acc[i1 / SPS][i1 % SPS];
                 tx_emit_off<OUT_MODE, OutT>(p, jt, jl + i, make_float2(a0.x, a0.y), make_float2(a1.x, a1.y), two);
+            }
+        }
+        __syncthreads();   // the window is restaged next trip
+    }
+}
+
+// ----------------------------------------------------------------------- TX on MFMA ----
+// The zero-stuffed polyphase FIR as f32 matrix products (v_mfma_f32_16x16x4_f32 is an exact
+// k-ordered fmaf chain, the same arithmetic as the VALU path, on the matrix pipe, leaving the
+// VALU to the bit-exact carrier phase, sin/cos and mix):
+//   rows i  = 16 row-blocks of SB = 16/SPS consecutive symbols,
+//   cols j  = (symbol c in the block, phase p) -> sample SPS*c + p of the block (16 samples),
+//   k  = o  = offset in a W = 4*NKS symbol window ending at the block's last symbol,
+//   A[i][o] = a[block_i - PRE + o]  (complex: one chain for re, one for im; from LDS),
+//   B[o][j] = h[p + SPS*(c + PRE - o)]  (banded tap matrix, constant: NKS VGPRs per lane).
+// MAC efficiency = (SB + K - 1) / W (0.92 for 129 taps at sps 4). One wave computes one
+// 16x16 output tile (256 samples) per 2*NKS MFMAs.
+template <int SPS> struct TxMfmaCfg {
+    static constexpr int SB = 16 / SPS;          // symbols per row-block
+    static constexpr int NT = 256;               // 4 waves
+    static constexpr int SUB = 4;                // 16x16 tiles per wave per tile
+    static constexpr int TS = 4 * SUB * 16 * SB; // symbols per workgroup tile
+};
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int SPS, int NKS, int OUT_MODE, typename OutT>
+__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const float* __restrict__ bfrag) {
+    using C = TxMfmaCfg<SPS>;
+    constexpr int SB = C::SB, NT = C::NT, SUB = C::SUB, TS = C::TS;
+    constexpr int PRE = 4 * NKS - SB;            // window symbols before a row-block
+    constexpr int NE = TS + PRE;                 // symbols staged per tile
+    constexpr int U = (NE + NT - 1) / NT;        // prefetched staging slots per lane
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2* lut_s = lds + ((NE + 1) & ~1);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x == 0) tx_state_update(p);
+    for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = p.lut[i];
+    float bf[NKS];                               // this lane's B fragments, one per k-step
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) bf[s] = bfrag[s * 64 + lane];
+
+    const int64_t ntiles = (p.nsym + TS - 1) / TS;
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    const bool pf = p.fast_bits != 0;
+    auto inside = [&](int64_t m0) { return pf && m0 - PRE >= 0 && m0 + TS <= p.nsym_valid; };
+    uint64_t pre[U];
+    auto prefetch = [&](int64_t m0) {
+        const int64_t mb = m0 - PRE;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = tid + NT * u;
+            pre[u] = tx_load_word(p.bits, p.bps, mb + (e < NE ? e : NE - 1));
+        }
+    };
+    if (t0 < t1 && inside(t0 * TS)) prefetch(t0 * TS);
+    __syncthreads();   // LUT visible
+
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t m0 = t * TS;
+        // 1. stage symbols m0-PRE .. m0+TS-1 -> lds[0 ..]
+        if (inside(m0)) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = tid + NT * u;
+                if (e < NE) lds[e] = lut_s[word_index(pre[u], p.bps)];
+            }
+        } else {
+            for (int e = tid; e < NE; e += NT) {
+                const int64_t m = m0 - PRE + e;
+                lds[e] = m < 0 ? (m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f))
+                               : (m >= p.nsym_valid ? make_float2(0.f, 0.f) : lut_s[tx_symbol_index(p, m)]);
+            }
+        }
+        __syncthreads();
+        if (t + 1 < t1 && inside(m0 + TS)) prefetch(m0 + TS);   // next bits fly meanwhile
+
+        // 2. SUB 16x16 output tiles per wave.
+        const int64_t jend = p.nsym * SPS;
+#pragma unroll 1
+        for (int q = 0; q < SUB; ++q) {
+            const int sb0 = (wave * SUB + q) * 16 * SB;            // first symbol of the tile
+            const float2* arow = lds + sb0 + SB * (lane & 15) + (lane >> 4);
+            f32x4 dre = {0.f, 0.f, 0.f, 0.f}, dim = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) {
+                const float2 a = arow[4 * s];
+                dre = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bf[s], dre, 0, 0, 0);
+                dim = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bf[s], dim, 0, 0, 0);
+            }
+            // D[row][col]: row = 4*(lane>>4) + r (row-block), col = lane & 15 (sample in block)
+            const int64_t jt = (m0 + sb0) * SPS;                   // first sample of the tile
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+                if (jt + off < jend)
+                    tx_emit_off<OUT_MODE, OutT>(p, jt, off, make_float2(dre[r], dim[r]),
+                                                make_float2(0.f, 0.f), false);
             }
         }
         __syncthreads();   // the window is restaged next trip
@@ -575,7 +685,11 @@ __device__ __forceinline__ void rx_stage_fast(const RxParams& p, float2* lds, in
             const int e = el + 2 * NT * u;
             if (e >= 0 && e < NS) {
                 float s, c;
+#ifdef MODEM_ABLATE_MIX
+                s = 0.f; c = (float)(nb32 + (uint32_t)e);
+#else
                 sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)e)), s, c);
+#endif
                 float2 z;
                 if (MIX == MIX_REFERENCE_REAL) z = make_float2(x[j].x * c, x[j].x * -s);
                 else z = make_float2(__builtin_fmaf(x[j].y, s, x[j].x * c),
@@ -653,6 +767,10 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
 #pragma unroll
             for (int i = 0; i < R; ++i) win[i] = ldc(base + i);
             int k = 0;
+#ifdef MODEM_ABLATE_FIR
+            k = K;
+            acc[0] += win[0];
+#endif
             for (; k + CH <= K; k += CH) {
                 const float2* pc = base - (k + CH);   // positive ds_read immediates
 #pragma unroll
@@ -876,6 +994,54 @@ static hipError_t tx_mode(const TxParams& p, int sps, int out_mode, hipStream_t 
     case OUT_IQ_BASEBAND: return tx_sps<OUT_IQ_BASEBAND, OutT>(p, sps, s);
     default: return tx_sps<OUT_REAL, OutT>(p, sps, s);
     }
+}
+
+template <int SPS, int NKS, int OM, typename OutT>
+static hipError_t txm_go(const TxParams& p, const float* bfrag, hipStream_t s) {
+    using C = TxMfmaCfg<SPS>;
+    constexpr int NE = C::TS + 4 * NKS - C::SB;
+    const int64_t ntiles = (p.nsym + C::TS - 1) / C::TS;
+    const size_t lds = ((size_t)((NE + 1) & ~1) + ((size_t)1 << p.bps)) * sizeof(float2);
+    const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT>);
+    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT>), dim3(persistent_grid(k, C::NT, lds, ntiles)),
+                       dim3(C::NT), lds, s, p, bfrag);
+    return hipGetLastError();
+}
+
+template <int OM, typename OutT>
+static hipError_t txm_sel(const TxParams& p, int sps, int nks, const float* bfrag, hipStream_t s) {
+#define TXM(S, N) if (sps == S && nks == N) return txm_go<S, N, OM, OutT>(p, bfrag, s);
+    TXM(4, 3) TXM(4, 5) TXM(4, 9) TXM(4, 17) TXM(4, 33)
+    TXM(8, 5) TXM(8, 9) TXM(8, 17) TXM(8, 33)
+    TXM(2, 5) TXM(2, 9) TXM(2, 17)
+    TXM(16, 3) TXM(16, 5) TXM(16, 9) TXM(16, 17)
+#undef TXM
+    return hipErrorInvalidValue;
+}
+
+int tx_mfma_ksteps(int sps, int K) {
+    if (sps != 2 && sps != 4 && sps != 8 && sps != 16) return 0;
+    const int need = (16 / sps + K - 1 + 3) / 4;
+    static const int steps[] = {3, 5, 9, 17, 33};
+    for (int n : steps) {
+        if (n < need) continue;
+        if ((sps == 8 && n == 3) || (sps == 2 && n == 3) || (sps == 2 && n == 33) || (sps == 16 && n == 33)) continue;
+        return n;
+    }
+    return 0;
+}
+
+hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const float* bfrag, int dtype, int out_mode,
+                          hipStream_t s) {
+    auto go = [&](auto outt) {
+        using OutT = decltype(outt);
+        switch (out_mode) {
+        case OUT_IQ_MIXED: return txm_sel<OUT_IQ_MIXED, OutT>(p, sps, nks, bfrag, s);
+        case OUT_IQ_BASEBAND: return txm_sel<OUT_IQ_BASEBAND, OutT>(p, sps, nks, bfrag, s);
+        default: return txm_sel<OUT_REAL, OutT>(p, sps, nks, bfrag, s);
+        }
+    };
+    return dtype == 1 ? go(__half()) : go(float());
 }
 
 hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s) {

@@ -51,9 +51,19 @@ def test_carrier_phase_bit_exact(m, o, torch_cuda, hz, sr, s0):
 
 
 # ------------------------------------------------------------------------ TX ----
+@pytest.fixture(params=["auto", "valu"])
+def fir_path(request, monkeypatch):
+    """TX FIR on the matrix pipe (default where instantiated) and forced onto the VALU."""
+    if request.param == "valu":
+        monkeypatch.setenv("MODEM_HIP_FIR", "valu")
+    else:
+        monkeypatch.delenv("MODEM_HIP_FIR", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("cfg", list(CONFIGS))
 @pytest.mark.parametrize("out_mode", [0, 1, 2])
-def test_tx_matches_oracle(m, o, torch_cuda, cfg, out_mode):
+def test_tx_matches_oracle(m, o, torch_cuda, cfg, out_mode, fir_path):
     name, bps, L, sps = CONFIGS[cfg]
     nsym = 3000
     bits = o.prng_bits(SEED + 1, nsym * bps)
@@ -78,8 +88,9 @@ def test_tx_sample_and_hold_bit_exact(m, o, torch_cuda, name, bps, sps):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("sps,L", [(3, 31), (5, 40), (45, 91), (16, 129), (2, 17), (1, 23)])
-def test_tx_other_rates(m, o, torch_cuda, sps, L):
+@pytest.mark.parametrize("sps,L", [(3, 31), (5, 40), (45, 91), (16, 129), (2, 17), (1, 23), (8, 129),
+                                   (4, 257), (4, 9), (2, 65), (16, 33)])
+def test_tx_other_rates(m, o, torch_cuda, sps, L, fir_path):
     """Generic and remaining specialised samples-per-symbol paths (e.g. sr/br = 45)."""
     bits = o.prng_bits(SEED + 3, 500 * 2)
     taps = m.rrc_taps(L, sps, 0.25)
@@ -90,7 +101,7 @@ def test_tx_other_rates(m, o, torch_cuda, sps, L):
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
-def test_tx_streaming_equals_one_call(m, o, torch_cuda):
+def test_tx_streaming_equals_one_call(m, o, torch_cuda, fir_path):
     """Ragged chunks (0, 1, non-multiples of bps) give the same samples as one call."""
     torch = torch_cuda
     name, bps, L, sps = CONFIGS["c3_qam16"]
@@ -123,7 +134,7 @@ def test_tx_host_buffers(m, o, torch_cuda):
     assert np.array_equal(dev, hst)
 
 
-def test_tx_f16(m, o, torch_cuda):
+def test_tx_f16(m, o, torch_cuda, fir_path):
     name, bps, L, sps = CONFIGS["c5_qam256"]
     bits = o.prng_bits(SEED + 6, 2000 * bps)
     taps = m.rrc_taps(L, sps, 0.35)
