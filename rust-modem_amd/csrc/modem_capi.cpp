@@ -462,6 +462,8 @@ struct modem_rx {
     uint64_t c0 = 0;
     int64_t consumed = 0;          // stream samples processed
     modem_slicer_desc slicer{};
+    int mfma_ksteps = 0;            // > 0: matched filter on the matrix pipe (rx_mfma)
+    float* d_bfrag = nullptr;       // its per-lane B fragments [ksteps][64]
     float* d_taps = nullptr;
     float2* d_slut = nullptr;
     void* d_hist[2] = {nullptr, nullptr};
@@ -470,7 +472,7 @@ struct modem_rx {
     Stage in_stage, iq_stage, sym_stage;
     ~modem_rx() {
         DeviceGuard g(device);
-        for (void* p : {(void*)d_taps, (void*)d_slut, d_hist[0], d_hist[1], d_zeros})
+        for (void* p : {(void*)d_taps, (void*)d_slut, d_hist[0], d_hist[1], d_zeros, (void*)d_bfrag})
             if (p) (void)hipFree(p);
     }
 };
@@ -531,6 +533,25 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
         hipMemcpy(h->d_slut, sl.lut, ((size_t)2 << sl.bits_per_symbol) * sizeof(float),
                   hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
+    }
+    const char* env = std::getenv("MODEM_HIP_FIR");
+    const bool force_valu = env && std::strcmp(env, "valu") == 0;
+    h->mfma_ksteps = force_valu ? 0 : mk::rx_mfma_ksteps((int)h->decim, (int)h->ntaps);
+    if (h->mfma_ksteps > 0) {
+        // B[w][c] = h[W - 1 - w - (15 - c)*decim] for lane l / k-step s: w = 4s + (l >> 4),
+        // c = l & 15 (rx_mfma in modem_kernels.hip).
+        const int nks = h->mfma_ksteps, W = 4 * nks, dec = (int)h->decim;
+        std::vector<float> bf((size_t)nks * 64, 0.0f);
+        for (int s2 = 0; s2 < nks; ++s2)
+            for (int l = 0; l < 64; ++l) {
+                const int wv = 4 * s2 + (l >> 4), c = l & 15;
+                const int u = W - 1 - wv - (15 - c) * dec;
+                if (u >= 0 && u < (int)h->ntaps) bf[(size_t)s2 * 64 + l] = d->taps[u];
+            }
+        if ((st = dalloc(&h->d_bfrag, bf.size()))) { delete h; return st; }
+        if (hipMemcpy(h->d_bfrag, bf.data(), bf.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
+        }
     }
     *out = h;
     return MODEM_OK;
@@ -600,7 +621,11 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
     p.inv_scale = h->slicer.inv_scale;
     p.max_symbol = h->slicer.max_symbol;
     p.w = h->w;
-    HIP_TRY(mk::launch_rx(p, (int)h->decim, h->in_dtype, h->out_dtype, h->mix, s));
+    if (h->mfma_ksteps > 0)
+        HIP_TRY(mk::launch_rx_mfma(p, (int)h->decim, h->mfma_ksteps, h->d_bfrag, h->in_dtype, h->out_dtype,
+                                   h->mix, s));
+    else
+        HIP_TRY(mk::launch_rx(p, (int)h->decim, h->in_dtype, h->out_dtype, h->mix, s));
     h->hcur ^= 1;
     h->consumed += (int64_t)n;
     if (host_iq) HIP_TRY(hipMemcpyAsync(out_iq, diq, (size_t)nout * rx_out_bytes(h), hipMemcpyDeviceToHost, s));

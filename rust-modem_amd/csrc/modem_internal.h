@@ -79,6 +79,10 @@ hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStr
 int tx_mfma_ksteps(int sps, int K);
 hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const float* bfrag, int dtype,
                           int out_mode, hipStream_t s);
+// RX matched filter on the matrix pipe (rx_mfma): ksteps for (decim, ntaps) or 0.
+int rx_mfma_ksteps(int decim, int L);
+hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const float* bfrag, int in_dtype,
+                          int out_dtype, int mix, hipStream_t s);
 hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,
                      hipStream_t s);
 hipError_t launch_fir(const FirParams& p, hipStream_t s);

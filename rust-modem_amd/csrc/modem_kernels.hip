@@ -796,6 +796,119 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
     }
 }
 
+// ----------------------------------------------------------------------- RX on MFMA ----
+// Matched filter at the kept instants as f32 matrix products (v_mfma_f32_16x16x4_f32):
+//   rows i = 16 groups of 16 consecutive kept instants, cols c = instant in the group,
+//   k = w  = offset in a W = 4*NKS sample window ending at the group's last instant,
+//   A[i][w] = z[start_i + w]  (mixed input from LDS; one chain for re, one for im),
+//   B[w][c] = h[W - 1 - w - (15 - c)*DEC]  (banded tap matrix: NKS VGPRs per lane).
+// MAC efficiency = L / W (0.67 for 129 taps at decimation 4). One wave: one 16x16 tile
+// (256 instants) per 2*NKS MFMAs. LDS keeps the mixed samples in natural order with 2 pad
+// samples after every RW = 16*DEC (one row of A), so the 16 rows of a read land in distinct
+// banks and every k-step is a compile-time immediate offset.
+template <int DEC> struct RxMfmaCfg {
+    static constexpr int NT = 256;               // 4 waves
+    static constexpr int TS = 4 * 256;           // kept instants per workgroup tile
+    static constexpr int RW = 16 * DEC;          // samples per A row
+};
+__host__ __device__ constexpr int rxm_pos(int e, int RW) { return e + 2 * (e / RW); }
+
+template <int DEC, int NKS, typename InT, int MIX, typename OutT>
+__global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const float* __restrict__ bfrag) {
+    using C = RxMfmaCfg<DEC>;
+    using IO = InIO<InT>;
+    using Raw = typename IO::Raw;
+    constexpr int NT = C::NT, TS = C::TS, RW = C::RW;
+    constexpr int W = 4 * NKS;
+    constexpr int NS = (TS - 16) * DEC + W;      // samples staged per tile
+    constexpr int U = (NS + 1 + 2 * NT - 1) / (2 * NT);
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x == 0) rx_state_update<InT>(p);
+    float bf[NKS];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) bf[s] = bfrag[s * 64 + lane];
+
+    const int64_t ntiles = (p.nout + TS - 1) / TS;
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    // tile t stages stream samples n_lo .. n_lo + NS - 1 (window start of its first row)
+    auto q_lo_of = [&](int64_t t) {
+        return (p.k_first + t * TS) * DEC + p.D + 15 * DEC - W + 1 - p.n_start;
+    };
+    const bool pf = p.x_aligned16 && p.small_n;
+    auto inside = [&](int64_t q_lo) {
+        const int64_t qb = q_lo - (q_lo & 1);
+        return pf && qb >= 0 && qb + 2 * NT * U <= p.N;
+    };
+    Raw pre[U];
+    auto prefetch = [&](int64_t q_lo) {
+        const Raw* xb = reinterpret_cast<const Raw*>(p.x) + ((q_lo - (q_lo & 1)) >> 1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) pre[u] = xb[tid + NT * u];
+    };
+    if (t0 < t1 && inside(q_lo_of(t0))) prefetch(q_lo_of(t0));
+
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t q_lo = q_lo_of(t);
+        const int64_t n_lo = q_lo + p.n_start;
+        // 1. mix the tile's samples into LDS (natural order, padded rows).
+        if (inside(q_lo)) {
+            const int par = (int)(q_lo & 1);
+            const uint32_t nb32 = (uint32_t)(p.c0 + (uint64_t)(n_lo - par));   // index of slot sample 0
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                float2 x[2];
+                IO::split(pre[u], x[0], x[1]);
+                const int e0 = 2 * (tid + NT * u) - par;     // stage index of x[0]
+                float2 z[2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    float s, c;
+                    sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j))), s, c);
+                    if (MIX == MIX_REFERENCE_REAL) z[j] = make_float2(x[j].x * c, x[j].x * -s);
+                    else z[j] = make_float2(__builtin_fmaf(x[j].y, s, x[j].x * c),
+                                            __builtin_fmaf(-x[j].x, s, x[j].y * c));
+                }
+                if (par == 0) {
+                    if (e0 < NS)   // pair never straddles a padded row (RW even): one 16-B store
+                        *reinterpret_cast<float4*>(lds + rxm_pos(e0, RW)) = make_float4(z[0].x, z[0].y, z[1].x, z[1].y);
+                } else {
+                    if (e0 >= 0 && e0 < NS) lds[rxm_pos(e0, RW)] = z[0];
+                    if (e0 + 1 < NS) lds[rxm_pos(e0 + 1, RW)] = z[1];
+                }
+            }
+        } else {
+            for (int e = tid; e < NS; e += NT)
+                lds[rxm_pos(e, RW)] = rx_mix<MIX>(p, n_lo, e, rx_sample<InT>(p, q_lo + e));
+        }
+        __syncthreads();
+        if (t + 1 < t1) {
+            const int64_t qn = q_lo_of(t + 1);
+            if (inside(qn)) prefetch(qn);          // next tile's samples fly during the MFMAs
+        }
+
+        // 2. one 16x16 tile per wave: instants kt + 16*i + c.
+        const int i = lane & 15, g = lane >> 4;
+        const float2* arow = lds + rxm_pos(wave * 16 * RW, RW) + i * (RW + 2) + g;
+        f32x4 dre = {0.f, 0.f, 0.f, 0.f}, dim = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const float2 a = arow[4 * s + 2 * ((4 * s) / RW)];
+            dre = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bf[s], dre, 0, 0, 0);
+            dim = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bf[s], dim, 0, 0, 0);
+        }
+        // D[row][col]: row = 4*g + r, col = i -> instant kt + 16*row + col
+        const float gain = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
+        const int64_t ot = t * TS + wave * 256;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t o = ot + 16 * (4 * g + r) + i;
+            if (o < p.nout) rx_emit<OutT>(p, o, gain * dre[r], gain * dim[r]);
+        }
+        __syncthreads();   // LDS is restaged next trip
+    }
+}
+
 // Any decimation: thread per kept instant, mixed samples staged in natural order.
 template <typename InT, int MIX, typename OutT>
 __global__ __launch_bounds__(64) void rx_generic(const RxParams p) {
@@ -1081,6 +1194,49 @@ template <typename InT, typename OutT>
 static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s) {
     return mix == MIX_REFERENCE_REAL ? rx_dec<InT, MIX_REFERENCE_REAL, OutT>(p, decim, s)
                                      : rx_dec<InT, MIX_COMPLEX, OutT>(p, decim, s);
+}
+
+template <int DEC, int NKS, typename InT, int MIX, typename OutT>
+static hipError_t rxm_go(const RxParams& p, const float* bfrag, hipStream_t s) {
+    using C = RxMfmaCfg<DEC>;
+    constexpr int NS = (C::TS - 16) * DEC + 4 * NKS;
+    const int64_t ntiles = (p.nout + C::TS - 1) / C::TS;
+    const size_t lds = ((size_t)rxm_pos(NS, C::RW) + 2) * sizeof(float2);
+    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT>);
+    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT>), dim3(persistent_grid(k, C::NT, lds, ntiles)),
+                       dim3(C::NT), lds, s, p, bfrag);
+    return hipGetLastError();
+}
+
+template <typename InT, int MIX, typename OutT>
+static hipError_t rxm_sel(const RxParams& p, int decim, int nks, const float* bfrag, hipStream_t s) {
+#define RXM(D, N) if (decim == D && nks == N) return rxm_go<D, N, InT, MIX, OutT>(p, bfrag, s);
+    RXM(4, 24) RXM(4, 32) RXM(4, 48) RXM(2, 16) RXM(2, 24) RXM(2, 40) RXM(8, 40) RXM(8, 48) RXM(8, 64)
+#undef RXM
+    return hipErrorInvalidValue;
+}
+
+int rx_mfma_ksteps(int decim, int L) {
+    const int need = (15 * decim + L + 3) / 4;
+    int cand[3] = {0, 0, 0};
+    if (decim == 4) { cand[0] = 24; cand[1] = 32; cand[2] = 48; }
+    else if (decim == 2) { cand[0] = 16; cand[1] = 24; cand[2] = 40; }
+    else if (decim == 8) { cand[0] = 40; cand[1] = 48; cand[2] = 64; }
+    for (int n : cand)
+        if (n >= need) return n;
+    return 0;
+}
+
+hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const float* bfrag, int in_dtype,
+                          int out_dtype, int mix, hipStream_t s) {
+    auto go = [&](auto in_t, auto out_t) {
+        using InT = decltype(in_t);
+        using OutT = decltype(out_t);
+        return mix == MIX_REFERENCE_REAL ? rxm_sel<InT, MIX_REFERENCE_REAL, OutT>(p, decim, nks, bfrag, s)
+                                         : rxm_sel<InT, MIX_COMPLEX, OutT>(p, decim, nks, bfrag, s);
+    };
+    if (in_dtype == 1) return out_dtype == 1 ? go(__half(), __half()) : go(__half(), float());
+    return out_dtype == 1 ? go(float(), __half()) : go(float(), float());
 }
 
 hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,

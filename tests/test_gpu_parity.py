@@ -146,7 +146,7 @@ def test_tx_f16(m, o, torch_cuda, fir_path):
 
 # ------------------------------------------------------------------------ RX ----
 @pytest.mark.parametrize("cfg", list(CONFIGS))
-def test_rx_matches_oracle(m, o, torch_cuda, cfg):
+def test_rx_matches_oracle(m, o, torch_cuda, cfg, fir_path):
     """Oracle TX samples in; decimated I/Q within tolerance, decisions bit-exact."""
     name, bps, L, sps = CONFIGS[cfg]
     nsym = 3000
@@ -166,7 +166,7 @@ def test_rx_matches_oracle(m, o, torch_cuda, cfg):
     assert np.array_equal(gsym[:nsym], sent_symbols(bits, bps))
 
 
-def test_rx_reference_demodulator(m, o, torch_cuda):
+def test_rx_reference_demodulator(m, o, torch_cuda, fir_path):
     """decim=1, real mix, 2x gain: Demodulator::next (demodulator.rs:44-56) at every sample."""
     rng = np.random.RandomState(11)
     n = 20000
@@ -184,7 +184,7 @@ def test_rx_reference_demodulator(m, o, torch_cuda):
     assert np.abs(giq - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
-def test_rx_streaming_equals_one_call(m, o, torch_cuda):
+def test_rx_streaming_equals_one_call(m, o, torch_cuda, fir_path):
     torch = torch_cuda
     name, bps, L, sps = CONFIGS["c3_qam16"]
     bits = o.prng_bits(SEED + 8, 5000 * bps)
@@ -224,7 +224,7 @@ def test_rx_flush_drains(m, o, torch_cuda):
     assert np.array_equal(got[:nsym], sent_symbols(bits, bps))
 
 
-def test_rx_f16_decisions(m, o, torch_cuda):
+def test_rx_f16_decisions(m, o, torch_cuda, fir_path):
     """C5 with f16 I/Q storage: samples within 2^-10, decisions bit-exact."""
     name, bps, L, sps = CONFIGS["c5_qam256"]
     nsym = 3000
@@ -238,8 +238,9 @@ def test_rx_f16_decisions(m, o, torch_cuda):
     assert np.array_equal(host(s)[:nsym], sent_symbols(bits, bps))
 
 
-@pytest.mark.parametrize("decim,L", [(3, 31), (45, 91), (16, 129), (2, 17)])
-def test_rx_other_rates(m, o, torch_cuda, decim, L):
+@pytest.mark.parametrize("decim,L", [(3, 31), (45, 91), (16, 129), (2, 17), (4, 33), (4, 65), (2, 65),
+                                     (2, 129), (8, 129), (8, 257), (4, 130)])
+def test_rx_other_rates(m, o, torch_cuda, decim, L, fir_path):
     name, bps = "qpsk", 2
     bits = o.prng_bits(SEED + 12, 400 * bps)
     taps = m.rrc_taps(L, decim, 0.25)
