@@ -412,82 +412,203 @@ template <int SPS> struct TxMfmaCfg {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Keep a loaded value in its register: an opaque asm use stops the compiler from
+// rematerialising the load inside the tile loop (where its vmcnt wait would also drain the
+// next tile's prefetch, since vector-memory counters retire in issue order).
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+
+// acc_re/acc_im += sum_s A_s * B_s over NKS k-steps; A_s (complex) is read from LDS at
+// arow[off(s)], PD k-steps ahead of its MFMA pair (explicit software pipeline: the
+// scheduling barriers keep the compiler from collapsing it to one read of look-ahead).
+template <int NKS, int PD, typename OffF>
+__device__ __forceinline__ void mfma_chain(const float2* arow, OffF off, const float (&bf)[NKS],
+                                           f32x4& dre, f32x4& dim) {
+#ifdef MODEM_ABLATE_FIR
+    const float2 a0 = arow[off(0)];
+    dre[0] += a0.x * bf[0]; dim[0] += a0.y * bf[NKS - 1];
+    return;
+#endif
+    float2 a[PD];
+#pragma unroll
+    for (int s = 0; s < PD && s < NKS; ++s) a[s] = arow[off(s)];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const float2 cur = a[s % PD];
+        if (s + PD < NKS) a[s % PD] = arow[off(s + PD)];
+        dre = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.x, bf[s], dre, 0, 0, 0);
+        dim = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.y, bf[s], dim, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int SPS, int NKS, int OUT_MODE, typename OutT>
+struct TxMfma {
+    using C = TxMfmaCfg<SPS>;
+    static constexpr int SB = C::SB, NT = C::NT, SUB = C::SUB, TS = C::TS;
+    static constexpr int PRE = 4 * NKS - SB;       // window symbols before a row-block
+    static constexpr int NE = TS + PRE;            // symbols staged per tile
+    static constexpr int U = (NE + NT - 1) / NT;   // prefetched staging slots per lane
+
+    // Raw bits word of symbol m, BPS bytes (fast path: aligned, no leftover bits).
+    template <int BPS>
+    __device__ static uint64_t load_word(const uint8_t* bits, int64_t m) {
+        const uint8_t* b = bits + m * BPS;
+        if (BPS == 1) return *b;
+        if (BPS == 2) return *reinterpret_cast<const uint16_t*>(b);
+        if (BPS == 4) return *reinterpret_cast<const uint32_t*>(b);
+        return *reinterpret_cast<const uint64_t*>(b);
+    }
+
+    // Slow staging: first tile (filter history), leftover bits, flush, any bps.
+    __device__ static void stage_slow(const TxParams& p, float2* lds, const float2* lut_s, int64_t m0) {
+        for (int e = threadIdx.x; e < NE; e += NT) {
+            const int64_t m = m0 - PRE + e;
+            lds[e] = m < 0 ? (m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f))
+                           : (m >= p.nsym_valid ? make_float2(0.f, 0.f) : lut_s[tx_symbol_index(p, m)]);
+        }
+    }
+
+    // FIR of this wave's sub-tile q: D = sum_s A_s B_s (see the comment above TxMfmaCfg).
+    __device__ static void fir(const float2* lds, int q, const float (&bf)[NKS], f32x4& dre, f32x4& dim) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int sb0 = (wave * SUB + q) * 16 * SB;
+        const float2* arow = lds + sb0 + SB * (lane & 15) + (lane >> 4);
+        dre = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dim = dre;
+        mfma_chain<NKS, 4>(arow, [](int s) { return 4 * s; }, bf, dre, dim);
+    }
+
+    // Full 16x16 tile, carrier index < 2^32: four independent chains, unconditional stores.
+    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim) {
+        const int lane = threadIdx.x & 63;
+        const uint32_t nb = (uint32_t)(p.s0 + (uint64_t)jt);
+        float zr[4], zi[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            zr[r] = dre[r];
+            zi[r] = dim[r];
+#ifdef MODEM_ABLATE_MIX
+            if (false) {
+#else
+            if (OUT_MODE != OUT_IQ_BASEBAND) {
+#endif
+                float sn, cs;
+                sincos_phase(phase_from_f(p.w, (float)(nb + (uint32_t)off)), sn, cs);
+                zr[r] = __builtin_fmaf(dre[r], cs, -(dim[r] * sn));
+                zi[r] = __builtin_fmaf(dre[r], sn, dim[r] * cs);
+            }
+        }
+#ifdef MODEM_ABLATE_STORE
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(zr[r]), "v"(zi[r]));
+#else
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t j = jt + 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, j, zr[r]);
+            else OutIO<OutT>::store_one(p.out, j, zr[r], zi[r]);
+        }
+#endif
+    }
+
+    // Partial tile or carrier index >= 2^32: guarded, 64-bit indices.
+    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim) {
+        const int lane = threadIdx.x & 63;
+        const int64_t jend = p.nsym * SPS;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            if (jt + off < jend)
+                tx_emit_off<OUT_MODE, OutT>(p, jt, off, make_float2(dre[r], dim[r]), make_float2(0.f, 0.f), false);
+        }
+    }
+
+    // BPS > 0: bits aligned, no leftover bits, carrier index < 2^32 (the steady state).
+    // BPS == 0: the general path (slow staging, guarded epilogue).
+    template <int BPS>
+    __device__ static void run(const TxParams& p, float2* lds, const float2* lut_s, const float (&bf)[NKS],
+                               int64_t t0, int64_t t1) {
+        const int tid = threadIdx.x;
+        const int64_t nfull = p.nsym / TS;          // tiles with every sample inside the call
+        const int64_t tf = BPS > 0 ? (t1 < nfull ? t1 : nfull) : t0;
+        const int64_t mlast = p.nsym_valid - 1;
+        auto inside = [&](int64_t m0) { return m0 - PRE >= 0 && m0 + TS <= p.nsym_valid; };
+        uint64_t pre[U];
+        // Always issued, address clamped into the call's bits: a fixed count of vector-memory
+        // operations per trip keeps the compiler's vmcnt waits counted (never vmcnt(0)).
+        auto prefetch = [&](int64_t m0) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int64_t m = m0 - PRE + tid + NT * u;
+                m = m < 0 ? 0 : (m > mlast ? mlast : m);
+                pre[u] = load_word<BPS>(p.bits, m);
+            }
+        };
+        if (BPS > 0 && t0 < tf && mlast >= 0) prefetch(t0 * TS);
+        for (int64_t t = t0; t < tf; ++t) {
+            const int64_t m0 = t * TS;
+            if (inside(m0)) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int e = tid + NT * u;
+                    if (e < NE) lds[e] = lut_s[word_index(pre[u], BPS)];
+                }
+            } else {
+                stage_slow(p, lds, lut_s, m0);
+            }
+            __syncthreads();
+            prefetch(m0 + TS);                       // next bits fly during the MFMAs
+            // fully unrolled: a static store count lets the next trip wait vmcnt(#stores)
+            // for its prefetched bits instead of draining this tile's stores
+#pragma unroll
+            for (int q = 0; q < SUB; ++q) {
+                f32x4 dre, dim;
+                fir(lds, q, bf, dre, dim);
+                emit_full(p, (m0 + ((threadIdx.x >> 6) * SUB + q) * 16 * SB) * SPS, dre, dim);
+            }
+            __syncthreads();                         // the window is restaged next trip
+        }
+        for (int64_t t = tf > t0 ? tf : t0; t < t1; ++t) {   // partial / general tiles
+            const int64_t m0 = t * TS;
+            stage_slow(p, lds, lut_s, m0);
+            __syncthreads();
+#pragma unroll 1
+            for (int q = 0; q < SUB; ++q) {
+                f32x4 dre, dim;
+                fir(lds, q, bf, dre, dim);
+                emit_edge(p, (m0 + ((threadIdx.x >> 6) * SUB + q) * 16 * SB) * SPS, dre, dim);
+            }
+            __syncthreads();
+        }
+    }
+};
+
 template <int SPS, int NKS, int OUT_MODE, typename OutT>
 __global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const float* __restrict__ bfrag) {
-    using C = TxMfmaCfg<SPS>;
-    constexpr int SB = C::SB, NT = C::NT, SUB = C::SUB, TS = C::TS;
-    constexpr int PRE = 4 * NKS - SB;            // window symbols before a row-block
-    constexpr int NE = TS + PRE;                 // symbols staged per tile
-    constexpr int U = (NE + NT - 1) / NT;        // prefetched staging slots per lane
+    using K = TxMfma<SPS, NKS, OUT_MODE, OutT>;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* lut_s = lds + ((NE + 1) & ~1);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    float2* lut_s = lds + ((K::NE + 1) & ~1);
+    const int tid = threadIdx.x, lane = tid & 63;
     if (blockIdx.x == 0) tx_state_update(p);
-    for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = p.lut[i];
+    for (int i = tid; i < (1 << p.bps); i += K::NT) lut_s[i] = p.lut[i];
     float bf[NKS];                               // this lane's B fragments, one per k-step
 #pragma unroll
     for (int s = 0; s < NKS; ++s) bf[s] = bfrag[s * 64 + lane];
-
-    const int64_t ntiles = (p.nsym + TS - 1) / TS;
-    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
-    const bool pf = p.fast_bits != 0;
-    auto inside = [&](int64_t m0) { return pf && m0 - PRE >= 0 && m0 + TS <= p.nsym_valid; };
-    uint64_t pre[U];
-    auto prefetch = [&](int64_t m0) {
-        const int64_t mb = m0 - PRE;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = tid + NT * u;
-            pre[u] = tx_load_word(p.bits, p.bps, mb + (e < NE ? e : NE - 1));
-        }
-    };
-    if (t0 < t1 && inside(t0 * TS)) prefetch(t0 * TS);
+    for (int s = 0; s < NKS; ++s) pin(bf[s]);
     __syncthreads();   // LUT visible
-
-    for (int64_t t = t0; t < t1; ++t) {
-        const int64_t m0 = t * TS;
-        // 1. stage symbols m0-PRE .. m0+TS-1 -> lds[0 ..]
-        if (inside(m0)) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = tid + NT * u;
-                if (e < NE) lds[e] = lut_s[word_index(pre[u], p.bps)];
-            }
-        } else {
-            for (int e = tid; e < NE; e += NT) {
-                const int64_t m = m0 - PRE + e;
-                lds[e] = m < 0 ? (m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f))
-                               : (m >= p.nsym_valid ? make_float2(0.f, 0.f) : lut_s[tx_symbol_index(p, m)]);
-            }
+    const int64_t ntiles = (p.nsym + K::TS - 1) / K::TS;
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    if (p.fast_bits && p.small_n) {              // one uniform switch: the tile loop is specialised
+        switch (p.bps) {
+        case 1: K::template run<1>(p, lds, lut_s, bf, t0, t1); return;
+        case 2: K::template run<2>(p, lds, lut_s, bf, t0, t1); return;
+        case 4: K::template run<4>(p, lds, lut_s, bf, t0, t1); return;
+        case 8: K::template run<8>(p, lds, lut_s, bf, t0, t1); return;
         }
-        __syncthreads();
-        if (t + 1 < t1 && inside(m0 + TS)) prefetch(m0 + TS);   // next bits fly meanwhile
-
-        // 2. SUB 16x16 output tiles per wave.
-        const int64_t jend = p.nsym * SPS;
-#pragma unroll 1
-        for (int q = 0; q < SUB; ++q) {
-            const int sb0 = (wave * SUB + q) * 16 * SB;            // first symbol of the tile
-            const float2* arow = lds + sb0 + SB * (lane & 15) + (lane >> 4);
-            f32x4 dre = {0.f, 0.f, 0.f, 0.f}, dim = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < NKS; ++s) {
-                const float2 a = arow[4 * s];
-                dre = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bf[s], dre, 0, 0, 0);
-                dim = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bf[s], dim, 0, 0, 0);
-            }
-            // D[row][col]: row = 4*(lane>>4) + r (row-block), col = lane & 15 (sample in block)
-            const int64_t jt = (m0 + sb0) * SPS;                   // first sample of the tile
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
-                if (jt + off < jend)
-                    tx_emit_off<OUT_MODE, OutT>(p, jt, off, make_float2(dre[r], dim[r]),
-                                                make_float2(0.f, 0.f), false);
-            }
-        }
-        __syncthreads();   // the window is restaged next trip
     }
+    K::template run<0>(p, lds, lut_s, bf, t0, t1);
 }
 
 // Any samples-per-symbol: thread per output sample, symbols staged in LDS.
@@ -618,6 +739,10 @@ __device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float i
 
 template <typename OutT>
 __device__ __forceinline__ void rx_emit(const RxParams& p, int64_t o, float re, float im) {
+#ifdef MODEM_ABLATE_STORE
+    asm volatile("" :: "v"(re), "v"(im));
+    return;
+#endif
     if (p.out_iq) OutIO<OutT>::store_one(p.out_iq, o, re, im);
     if (p.out_sym && p.slicer_kind != SLICER_NONE) p.out_sym[o] = rx_slice(p, re, im);
 }
@@ -828,6 +953,8 @@ __global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const float* __
     float bf[NKS];
 #pragma unroll
     for (int s = 0; s < NKS; ++s) bf[s] = bfrag[s * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) pin(bf[s]);
 
     const int64_t ntiles = (p.nout + TS - 1) / TS;
     const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
@@ -864,17 +991,24 @@ __global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const float* __
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     float s, c;
+#ifdef MODEM_ABLATE_MIX
+                    s = 0.f; c = (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j));
+#else
                     sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j))), s, c);
+#endif
                     if (MIX == MIX_REFERENCE_REAL) z[j] = make_float2(x[j].x * c, x[j].x * -s);
                     else z[j] = make_float2(__builtin_fmaf(x[j].y, s, x[j].x * c),
                                             __builtin_fmaf(-x[j].x, s, x[j].y * c));
                 }
+                // Only the first and last slots can fall outside [0, NS): the other guards
+                // are compile-time true, so the slots' chains interleave without branches.
+                const bool last = (u + 1) * 2 * NT > NS - 1;
                 if (par == 0) {
-                    if (e0 < NS)   // pair never straddles a padded row (RW even): one 16-B store
+                    if (!last || e0 < NS)   // pair never straddles a padded row (RW even): one 16-B store
                         *reinterpret_cast<float4*>(lds + rxm_pos(e0, RW)) = make_float4(z[0].x, z[0].y, z[1].x, z[1].y);
                 } else {
-                    if (e0 >= 0 && e0 < NS) lds[rxm_pos(e0, RW)] = z[0];
-                    if (e0 + 1 < NS) lds[rxm_pos(e0 + 1, RW)] = z[1];
+                    if ((u > 0 || e0 >= 0) && (!last || e0 < NS)) lds[rxm_pos(e0, RW)] = z[0];
+                    if (!last || e0 + 1 < NS) lds[rxm_pos(e0 + 1, RW)] = z[1];
                 }
             }
         } else {
@@ -891,12 +1025,7 @@ __global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const float* __
         const int i = lane & 15, g = lane >> 4;
         const float2* arow = lds + rxm_pos(wave * 16 * RW, RW) + i * (RW + 2) + g;
         f32x4 dre = {0.f, 0.f, 0.f, 0.f}, dim = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < NKS; ++s) {
-            const float2 a = arow[4 * s + 2 * ((4 * s) / RW)];
-            dre = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bf[s], dre, 0, 0, 0);
-            dim = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bf[s], dim, 0, 0, 0);
-        }
+        mfma_chain<NKS, 4>(arow, [](int s) { return 4 * s + 2 * ((4 * s) / RW); }, bf, dre, dim);
         // D[row][col]: row = 4*g + r, col = i -> instant kt + 16*row + col
         const float gain = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
         const int64_t ot = t * TS + wave * 256;
@@ -1112,7 +1241,7 @@ static hipError_t tx_mode(const TxParams& p, int sps, int out_mode, hipStream_t 
 template <int SPS, int NKS, int OM, typename OutT>
 static hipError_t txm_go(const TxParams& p, const float* bfrag, hipStream_t s) {
     using C = TxMfmaCfg<SPS>;
-    constexpr int NE = C::TS + 4 * NKS - C::SB;
+    constexpr int NE = TxMfma<SPS, NKS, OM, OutT>::NE;
     const int64_t ntiles = (p.nsym + C::TS - 1) / C::TS;
     const size_t lds = ((size_t)((NE + 1) & ~1) + ((size_t)1 << p.bps)) * sizeof(float2);
     const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT>);

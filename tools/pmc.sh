@@ -11,6 +11,7 @@ groups=(
   "FETCH_SIZE"
   "WRITE_SIZE"
   "TCC_HIT_sum TCC_MISS_sum"
+  "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_F32"
 )
 i=0
 for g in "${groups[@]}"; do
