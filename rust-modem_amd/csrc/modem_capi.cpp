@@ -463,7 +463,7 @@ struct modem_rx {
     int64_t consumed = 0;          // stream samples processed
     modem_slicer_desc slicer{};
     int mfma_ksteps = 0;            // > 0: matched filter on the matrix pipe (rx_mfma)
-    float* d_bfrag = nullptr;       // its per-lane B fragments [ksteps][64]
+    float* d_bfrag = nullptr;       // its reversed-tap band table (rx_mfma_table_len floats)
     float* d_taps = nullptr;
     float2* d_slut = nullptr;
     void* d_hist[2] = {nullptr, nullptr};
@@ -538,16 +538,15 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
     const bool force_valu = env && std::strcmp(env, "valu") == 0;
     h->mfma_ksteps = force_valu ? 0 : mk::rx_mfma_ksteps((int)h->decim, (int)h->ntaps);
     if (h->mfma_ksteps > 0) {
-        // B[w][c] = h[W - 1 - w - (15 - c)*decim] for lane l / k-step s: w = 4s + (l >> 4),
-        // c = l & 15 (rx_mfma in modem_kernels.hip).
+        // B[w][c] = h[W - 1 - w - (15 - c)*decim] is a Toeplitz band: lane (g, c) at k-step s
+        // (w = 4s + g) reads T[4s + g + (15 - c)*decim] of the reversed, zero-padded taps
+        // T[j] = h[W - 1 - j] (rx_mfma stages T in LDS; modem_kernels.hip).
         const int nks = h->mfma_ksteps, W = 4 * nks, dec = (int)h->decim;
-        std::vector<float> bf((size_t)nks * 64, 0.0f);
-        for (int s2 = 0; s2 < nks; ++s2)
-            for (int l = 0; l < 64; ++l) {
-                const int wv = 4 * s2 + (l >> 4), c = l & 15;
-                const int u = W - 1 - wv - (15 - c) * dec;
-                if (u >= 0 && u < (int)h->ntaps) bf[(size_t)s2 * 64 + l] = d->taps[u];
-            }
+        std::vector<float> bf((size_t)mk::rx_mfma_table_len(dec, nks), 0.0f);
+        for (int j = 0; j < W + 15 * dec; ++j) {
+            const int u = W - 1 - j;
+            if (u >= 0 && u < (int)h->ntaps) bf[(size_t)j] = d->taps[u];
+        }
         if ((st = dalloc(&h->d_bfrag, bf.size()))) { delete h; return st; }
         if (hipMemcpy(h->d_bfrag, bf.data(), bf.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;

@@ -81,6 +81,8 @@ hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const float* bfra
                           int out_mode, hipStream_t s);
 // RX matched filter on the matrix pipe (rx_mfma): ksteps for (decim, ntaps) or 0.
 int rx_mfma_ksteps(int decim, int L);
+// Floats in its band table T[j] = h[W - 1 - j], j < 4*nks + 15*decim (rounded up to 4).
+constexpr int rx_mfma_table_len(int decim, int nks) { return (4 * nks + 15 * decim + 3) & ~3; }
 hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const float* bfrag, int in_dtype,
                           int out_dtype, int mix, hipStream_t s);
 hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,

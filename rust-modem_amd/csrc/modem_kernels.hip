@@ -441,6 +441,37 @@ __device__ __forceinline__ void mfma_chain(const float2* arow, OffF off, const f
     }
 }
 
+// The same chain with B also read from LDS, at brow[4*s] (a Toeplitz band table: one
+// conflict-free ds_read_b32 per k-step instead of NKS fragment registers per lane).
+template <int NKS, int PD, typename OffF>
+__device__ __forceinline__ void mfma_chain_lb(const float2* arow, OffF off, const float* brow,
+                                              f32x4& dre, f32x4& dim) {
+#ifdef MODEM_ABLATE_FIR
+    const float2 a0 = arow[off(0)];
+    dre[0] += a0.x * brow[0]; dim[0] += a0.y * brow[4];
+    return;
+#endif
+    float2 a[PD];
+    float b[PD];
+#pragma unroll
+    for (int s = 0; s < PD && s < NKS; ++s) {
+        a[s] = arow[off(s)];
+        b[s] = brow[4 * s];
+    }
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const float2 cur = a[s % PD];
+        const float cb = b[s % PD];
+        if (s + PD < NKS) {
+            a[s % PD] = arow[off(s + PD)];
+            b[s % PD] = brow[4 * (s + PD)];
+        }
+        dre = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.x, cb, dre, 0, 0, 0);
+        dim = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.y, cb, dim, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 template <int SPS, int NKS, int OUT_MODE, typename OutT>
 struct TxMfma {
     using C = TxMfmaCfg<SPS>;
@@ -938,104 +969,199 @@ template <int DEC> struct RxMfmaCfg {
 };
 __host__ __device__ constexpr int rxm_pos(int e, int RW) { return e + 2 * (e / RW); }
 
+// What the steady-state epilogue writes: baseband IQ, QAM-axis decisions, or both
+// (RXE_GEN: any other combination, guarded per store).
+enum { RXE_GEN = 0, RXE_IQ = 1, RXE_SYM = 2, RXE_IQSYM = 3 };
+
+__device__ __forceinline__ uint8_t rx_slice_qam(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    const int ms = (int)p.max_symbol;
+    const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
+    const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
+    int si = (int)__builtin_rintf(fi), sq = (int)__builtin_rintf(fq);
+    si = si < 0 ? 0 : (si > ms ? ms : si);
+    sq = sq < 0 ? 0 : (sq > ms ? ms : sq);
+    return (uint8_t)((si << p.bits_per_carrier) | sq);
+}
+
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
-__global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const float* __restrict__ bfrag) {
+struct RxMfma {
     using C = RxMfmaCfg<DEC>;
     using IO = InIO<InT>;
     using Raw = typename IO::Raw;
-    constexpr int NT = C::NT, TS = C::TS, RW = C::RW;
-    constexpr int W = 4 * NKS;
-    constexpr int NS = (TS - 16) * DEC + W;      // samples staged per tile
-    constexpr int U = (NS + 1 + 2 * NT - 1) / (2 * NT);
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (blockIdx.x == 0) rx_state_update<InT>(p);
-    float bf[NKS];
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) bf[s] = bfrag[s * 64 + lane];
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) pin(bf[s]);
+    static constexpr int NT = C::NT, TS = C::TS, RW = C::RW;
+    static constexpr int W = 4 * NKS;
+    static constexpr int NS = (TS - 16) * DEC + W;            // samples staged per tile
+    static constexpr int U = (NS + 1 + 2 * NT - 1) / (2 * NT); // prefetched sample pairs per lane
+    static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
 
-    const int64_t ntiles = (p.nout + TS - 1) / TS;
-    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
-    // tile t stages stream samples n_lo .. n_lo + NS - 1 (window start of its first row)
-    auto q_lo_of = [&](int64_t t) {
+    // Tile t stages chunk samples q_lo .. q_lo + NS - 1 (window start of its first row).
+    __device__ static int64_t q_lo_of(const RxParams& p, int64_t t) {
         return (p.k_first + t * TS) * DEC + p.D + 15 * DEC - W + 1 - p.n_start;
-    };
-    const bool pf = p.x_aligned16 && p.small_n;
-    auto inside = [&](int64_t q_lo) {
-        const int64_t qb = q_lo - (q_lo & 1);
-        return pf && qb >= 0 && qb + 2 * NT * U <= p.N;
-    };
-    Raw pre[U];
-    auto prefetch = [&](int64_t q_lo) {
-        const Raw* xb = reinterpret_cast<const Raw*>(p.x) + ((q_lo - (q_lo & 1)) >> 1);
-#pragma unroll
-        for (int u = 0; u < U; ++u) pre[u] = xb[tid + NT * u];
-    };
-    if (t0 < t1 && inside(q_lo_of(t0))) prefetch(q_lo_of(t0));
+    }
 
-    for (int64_t t = t0; t < t1; ++t) {
-        const int64_t q_lo = q_lo_of(t);
-        const int64_t n_lo = q_lo + p.n_start;
-        // 1. mix the tile's samples into LDS (natural order, padded rows).
-        if (inside(q_lo)) {
-            const int par = (int)(q_lo & 1);
-            const uint32_t nb32 = (uint32_t)(p.c0 + (uint64_t)(n_lo - par));   // index of slot sample 0
+    // Steady state: the tile's samples are whole pairs of this chunk, carrier index < 2^32,
+    // every instant is kept. PAR = q_lo & 1 is the same for every tile of a call (TS*DEC even).
+    template <int PAR>
+    __device__ static void stage_fast(const RxParams& p, float2* lds, uint32_t nb32, const Raw (&pre)[U]) {
+        const int tid = threadIdx.x;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                float2 x[2];
-                IO::split(pre[u], x[0], x[1]);
-                const int e0 = 2 * (tid + NT * u) - par;     // stage index of x[0]
-                float2 z[2];
+        for (int u = 0; u < U; ++u) {
+            float2 x[2];
+            IO::split(pre[u], x[0], x[1]);
+            const int e0 = 2 * (tid + NT * u) - PAR;     // stage index of x[0]
+            float2 z[2];
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    float s, c;
+            for (int j = 0; j < 2; ++j) {
+                float sn, cs;
 #ifdef MODEM_ABLATE_MIX
-                    s = 0.f; c = (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j));
+                sn = 0.f; cs = (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j));
 #else
-                    sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j))), s, c);
+                sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j))), sn, cs);
 #endif
-                    if (MIX == MIX_REFERENCE_REAL) z[j] = make_float2(x[j].x * c, x[j].x * -s);
-                    else z[j] = make_float2(__builtin_fmaf(x[j].y, s, x[j].x * c),
-                                            __builtin_fmaf(-x[j].x, s, x[j].y * c));
-                }
-                // Only the first and last slots can fall outside [0, NS): the other guards
-                // are compile-time true, so the slots' chains interleave without branches.
-                const bool last = (u + 1) * 2 * NT > NS - 1;
-                if (par == 0) {
-                    if (!last || e0 < NS)   // pair never straddles a padded row (RW even): one 16-B store
-                        *reinterpret_cast<float4*>(lds + rxm_pos(e0, RW)) = make_float4(z[0].x, z[0].y, z[1].x, z[1].y);
-                } else {
-                    if ((u > 0 || e0 >= 0) && (!last || e0 < NS)) lds[rxm_pos(e0, RW)] = z[0];
-                    if (!last || e0 + 1 < NS) lds[rxm_pos(e0 + 1, RW)] = z[1];
-                }
+                if (MIX == MIX_REFERENCE_REAL) z[j] = make_float2(x[j].x * cs, x[j].x * -sn);
+                else z[j] = make_float2(__builtin_fmaf(x[j].y, sn, x[j].x * cs),
+                                        __builtin_fmaf(-x[j].x, sn, x[j].y * cs));
             }
-        } else {
-            for (int e = tid; e < NS; e += NT)
-                lds[rxm_pos(e, RW)] = rx_mix<MIX>(p, n_lo, e, rx_sample<InT>(p, q_lo + e));
+            // Only the first and last slots can fall outside [0, NS): the other guards are
+            // compile-time true, so the slots' chains interleave without branches.
+            const bool last = (u + 1) * 2 * NT > NS - 1;
+            if (PAR == 0) {
+                if (!last || e0 < NS)   // a pair never straddles a padded row (RW even): one 16-B store
+                    *reinterpret_cast<float4*>(lds + rxm_pos(e0, RW)) = make_float4(z[0].x, z[0].y, z[1].x, z[1].y);
+            } else {
+                if ((u > 0 || e0 >= 0) && (!last || e0 < NS)) lds[rxm_pos(e0, RW)] = z[0];
+                if (!last || e0 + 1 < NS) lds[rxm_pos(e0 + 1, RW)] = z[1];
+            }
         }
-        __syncthreads();
-        if (t + 1 < t1) {
-            const int64_t qn = q_lo_of(t + 1);
-            if (inside(qn)) prefetch(qn);          // next tile's samples fly during the MFMAs
-        }
+    }
 
-        // 2. one 16x16 tile per wave: instants kt + 16*i + c.
-        const int i = lane & 15, g = lane >> 4;
-        const float2* arow = lds + rxm_pos(wave * 16 * RW, RW) + i * (RW + 2) + g;
-        f32x4 dre = {0.f, 0.f, 0.f, 0.f}, dim = {0.f, 0.f, 0.f, 0.f};
-        mfma_chain<NKS, 4>(arow, [](int s) { return 4 * s + 2 * ((4 * s) / RW); }, bf, dre, dim);
-        // D[row][col]: row = 4*g + r, col = i -> instant kt + 16*row + col
-        const float gain = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
-        const int64_t ot = t * TS + wave * 256;
+    // First / last tiles of a chunk, unaligned input, carrier index >= 2^32: per sample.
+    __device__ static void stage_slow(const RxParams& p, float2* lds, int64_t q_lo) {
+        const int64_t n_lo = q_lo + p.n_start;
+        for (int e = threadIdx.x; e < NS; e += NT)
+            lds[rxm_pos(e, RW)] = rx_mix<MIX>(p, n_lo, e, rx_sample<InT>(p, q_lo + e));
+    }
+
+    static constexpr int TBL = rx_mfma_table_len(DEC, NKS);   // band table floats
+    static constexpr int LDS_SAMPLES = rxm_pos(NS, RW) + 2;      // float2 slots before the table
+
+    // One 16x16 tile per wave: instants kt + 16*i + c. Lane (g, c) reads A from row c of its
+    // wave's block and B[4s + g][c] = T[4s + g + (15 - c)*DEC] from the band table.
+    __device__ static void fir(const float2* lds, const float* tbl, f32x4& dre, f32x4& dim) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const float2* arow = lds + rxm_pos(wave * 16 * RW, RW) + (lane & 15) * (RW + 2) + (lane >> 4);
+        const float* brow = tbl + (lane >> 4) + (15 - (lane & 15)) * DEC;
+        dre = (f32x4){0.f, 0.f, 0.f, 0.f};
+        dim = dre;
+        mfma_chain_lb<NKS, 4>(arow, [](int s) { return 4 * s + 2 * ((4 * s) / RW); }, brow, dre, dim);
+    }
+
+    // D[row][col]: row = 4*(lane>>4) + r, col = lane&15 -> instant ot + 16*row + col.
+    template <int EM>
+    __device__ static void emit_full(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim) {
+        const int lane = threadIdx.x & 63;
+#ifdef MODEM_ABLATE_STORE
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(dre[r]), "v"(dim[r]));
+        return;
+#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int64_t o = ot + 16 * (4 * g + r) + i;
-            if (o < p.nout) rx_emit<OutT>(p, o, gain * dre[r], gain * dim[r]);
+            const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            const float re = GAIN * dre[r], im = GAIN * dim[r];
+            if (EM == RXE_GEN) {
+                rx_emit<OutT>(p, ot + off, re, im);
+                continue;
+            }
+            if (EM & RXE_IQ) OutIO<OutT>::store_one(p.out_iq, ot + off, re, im);
+            if (EM & RXE_SYM) p.out_sym[ot + off] = rx_slice_qam(p, re, im);
         }
-        __syncthreads();   // LDS is restaged next trip
     }
+
+    __device__ static void emit_edge(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim) {
+        const int lane = threadIdx.x & 63;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t o = ot + 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            if (o < p.nout) rx_emit<OutT>(p, o, GAIN * dre[r], GAIN * dim[r]);
+        }
+    }
+
+    // Tiles of [t0, t1). When the call's input is 16-B aligned and its carrier indices stay
+    // below 2^32, the run of "full" tiles (all staged samples inside the chunk, all 1024
+    // instants kept) goes through the prefetched loop, whose epilogue EM stores unconditionally;
+    // the first and last tiles of the chunk take the general path. PAR = q_lo & 1 is the same
+    // for every tile of a call (TS*DEC is even).
+    template <int EM>
+    __device__ static void run(const RxParams& p, float2* lds, const float* bf, int64_t t0, int64_t t1) {
+        const int tid = threadIdx.x, wave = tid >> 6;
+        const int64_t npairs = p.N >> 1;
+        const bool fast = p.x_aligned16 && p.small_n;
+        const int PAR = (int)(q_lo_of(p, 0) & 1);
+        auto full = [&](int64_t t) {
+            const int64_t qb = q_lo_of(p, t) - PAR;
+            return fast && qb >= 0 && qb + 2 * NT * U <= p.N && (t + 1) * TS <= p.nout;
+        };
+        Raw pre[U];
+        // Always issued, base clamped into the chunk: a fixed count of vector-memory operations
+        // per trip keeps the compiler's vmcnt waits counted (a non-full next tile is restaged).
+        auto prefetch = [&](int64_t t) {
+            int64_t base = (q_lo_of(p, t) - PAR) >> 1;
+            base = base > npairs - NT * U ? npairs - NT * U : base;
+            const Raw* xb = reinterpret_cast<const Raw*>(p.x) + base;
+#pragma unroll
+            for (int u = 0; u < U; ++u) pre[u] = xb[tid + NT * u];
+        };
+        int64_t t = t0;
+        while (t < t1) {
+            if (full(t)) {
+                prefetch(t);
+                for (; t < t1 && full(t); ++t) {
+                    const int64_t n_lo = q_lo_of(p, t) + p.n_start;
+                    const uint32_t nb32 = (uint32_t)(p.c0 + (uint64_t)(n_lo - PAR));
+                    if (PAR) stage_fast<1>(p, lds, nb32, pre);   // uniform; no memory-counter ops inside
+                    else stage_fast<0>(p, lds, nb32, pre);
+                    __syncthreads();
+                    prefetch(t + 1);                       // next samples fly during the MFMAs
+                    f32x4 dre, dim;
+                    fir(lds, bf, dre, dim);
+                    emit_full<EM>(p, t * TS + wave * 256, dre, dim);
+                    __syncthreads();                       // LDS is restaged next trip
+                }
+            } else {
+                stage_slow(p, lds, q_lo_of(p, t));
+                __syncthreads();
+                f32x4 dre, dim;
+                fir(lds, bf, dre, dim);
+                emit_edge(p, t * TS + wave * 256, dre, dim);
+                __syncthreads();
+                ++t;
+            }
+        }
+    }
+};
+
+template <int DEC, int NKS, typename InT, int MIX, typename OutT>
+__global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const float* __restrict__ bfrag) {
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    if (blockIdx.x == 0) rx_state_update<InT>(p);
+    float* bf = reinterpret_cast<float*>(lds + K::LDS_SAMPLES);   // band table, read-only below
+    for (int j = threadIdx.x; j < K::TBL; j += K::NT) bf[j] = bfrag[j];
+    __syncthreads();
+    const int64_t ntiles = (p.nout + K::TS - 1) / K::TS;
+    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    if (t0 >= t1) return;
+    // f32 input with the complex mix (the loopback chain): the epilogue is specialised on what
+    // it stores, so the tile loop's store count is static. Other variants share the guarded one.
+    if (std::is_same<InT, float>::value && MIX == MIX_COMPLEX) {
+        const bool qam = p.slicer_kind == SLICER_QAM_AXIS && p.out_sym;
+        if (p.out_iq && qam) { K::template run<RXE_IQSYM>(p, lds, bf, t0, t1); return; }
+        if (p.out_iq && !p.out_sym) { K::template run<RXE_IQ>(p, lds, bf, t0, t1); return; }
+        if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, lds, bf, t0, t1); return; }
+    }
+    K::template run<RXE_GEN>(p, lds, bf, t0, t1);
 }
 
 // Any decimation: thread per kept instant, mixed samples staged in natural order.
@@ -1328,9 +1454,9 @@ static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
 static hipError_t rxm_go(const RxParams& p, const float* bfrag, hipStream_t s) {
     using C = RxMfmaCfg<DEC>;
-    constexpr int NS = (C::TS - 16) * DEC + 4 * NKS;
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
     const int64_t ntiles = (p.nout + C::TS - 1) / C::TS;
-    const size_t lds = ((size_t)rxm_pos(NS, C::RW) + 2) * sizeof(float2);
+    const size_t lds = (size_t)K::LDS_SAMPLES * sizeof(float2) + (size_t)K::TBL * sizeof(float);
     const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT>);
     hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT>), dim3(persistent_grid(k, C::NT, lds, ntiles)),
                        dim3(C::NT), lds, s, p, bfrag);
