@@ -54,6 +54,11 @@ def algorithmic_bytes(bps, ntaps, sps, nsamp, dtype):
     return tx, rx, nout
 
 
+def channel_seed(rank, nch, c):
+    """Channel c of rank `rank`: every rank owns distinct channels (weak scaling, no exchange)."""
+    return SEED + rank * nch + c
+
+
 class GpuRunner:
     """The product path: rust_modem_amd handles on this rank's GPU, buffers resident in HBM."""
 
@@ -73,7 +78,7 @@ class GpuRunner:
         self.ch = []
         nbits = nsamp // sps * bps
         for c in range(nch):
-            seed = SEED + rank * nch + c
+            seed = channel_seed(rank, nch, c)
             bits = m.prng_bits(seed, nbits, device=device)
             tx = m.DigitalModulator(m.Carrier(w), ph(), sps, taps, dtype=dtype)
             rx = m.DemodulatorRx(m.Carrier(w), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,

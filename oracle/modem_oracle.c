@@ -436,9 +436,9 @@ uint8_t or_slice(const or_slicer* s, float re, float im) {
         int ms = (int)s->max_symbol;
         float fi = (re * s->inv_scale + s->max_symbol) * 0.5f;
         float fq = (im * s->inv_scale + s->max_symbol) * 0.5f;
-        int si = (int)rintf(fi), sq = (int)rintf(fq);
-        si = si < 0 ? 0 : (si > ms ? ms : si);
-        sq = sq < 0 ? 0 : (sq > ms ? ms : sq);
+        /* clamp before the conversion: huge / NaN inputs stay defined (fmaxf drops a NaN) */
+        int si = (int)fminf(fmaxf(rintf(fi), 0.0f), (float)ms);
+        int sq = (int)fminf(fmaxf(rintf(fq), 0.0f), (float)ms);
         return (uint8_t)((si << s->bits_per_carrier) | sq);
     }
     size_t n = (size_t)1 << s->bps;

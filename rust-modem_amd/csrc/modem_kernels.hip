@@ -751,9 +751,8 @@ __device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float i
         const int ms = (int)p.max_symbol;
         const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
         const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
-        int si = (int)__builtin_rintf(fi), sq = (int)__builtin_rintf(fq);
-        si = si < 0 ? 0 : (si > ms ? ms : si);
-        sq = sq < 0 ? 0 : (sq > ms ? ms : sq);
+        const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), (float)ms);
+        const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), (float)ms);
         return (uint8_t)((si << p.bits_per_carrier) | sq);
     }
     cfloat* lut = (cfloat*)p.slut;
@@ -978,9 +977,9 @@ __device__ __forceinline__ uint8_t rx_slice_qam(const RxParams& p, float re, flo
     const int ms = (int)p.max_symbol;
     const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
     const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
-    int si = (int)__builtin_rintf(fi), sq = (int)__builtin_rintf(fq);
-    si = si < 0 ? 0 : (si > ms ? ms : si);
-    sq = sq < 0 ? 0 : (sq > ms ? ms : sq);
+    // clamp before the conversion: huge / NaN inputs stay defined (fmax drops a NaN)
+    const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), (float)ms);
+    const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), (float)ms);
     return (uint8_t)((si << p.bits_per_carrier) | sq);
 }
 

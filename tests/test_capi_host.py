@@ -1,0 +1,196 @@
+"""The C-ABI library on the CPU: it loads, exports every entry point include/modem_hip.h
+declares, and its host-side logic (timebase, phasor tables, slicer, taps, status codes,
+argument checks) equals the oracle. No compute call reaches a device here: device entry
+points must fail with a status (MODEM_ERR_NO_DEVICE), never crash.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import PI_4, ROOT
+
+HEADER = os.path.join(ROOT, "include", "modem_hip.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    return sorted(set(re.findall(r"\b(modem_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ("modem_tx_create", "modem_tx_process", "modem_tx_flush", "modem_tx_destroy",
+                     "modem_rx_create", "modem_rx_process", "modem_rx_flush", "modem_rx_destroy",
+                     "modem_fir_create", "modem_fir_process", "modem_fir_destroy", "modem_status_str",
+                     "modem_phasor_lut", "modem_carrier_phase"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol(m):
+    lib = ctypes.CDLL(m.lib_path())
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, f"declared in modem_hip.h but not exported: {missing}"
+
+
+def test_abi_version(m):
+    text = open(HEADER).read()
+    want = int(re.search(r"#define MODEM_HIP_ABI_VERSION (\d+)", text).group(1))
+    assert m.load_library().modem_abi_version() == want
+
+
+def test_status_strings(m):
+    for s in (0, -1, -2, -3, -4, -5, -6):
+        assert m.status_str(s) and "unknown" not in m.status_str(s).lower()
+    assert m.status_str(-99)
+
+
+def test_product_never_loads_the_oracle(m):
+    """The product library links nothing from oracle/ (the checker stays test-only)."""
+    import subprocess
+    out = subprocess.run(["readelf", "-d", m.lib_path()], capture_output=True, text=True).stdout
+    assert "modem_oracle" not in out
+    syms = subprocess.run(["nm", "-D", m.lib_path()], capture_output=True, text=True).stdout
+    assert " or_" not in syms
+
+
+# --------------------------------------------------------------- host-side logic ----
+@pytest.mark.parametrize("hz,sr", [(1, 4), (1000, 10000), (1200, 48000), (0, 8)])
+def test_freq_sample_freq(m, o, hz, sr):
+    """freq.rs:19-26 bit-exact."""
+    assert np.float32(m.Freq(hz, sr).sample_freq()) == np.float32(o.sample_freq(hz, sr))
+
+
+def test_rates(m, o):
+    """rates.rs: samples_per_symbol = sr / br; br = 0 panics (divide by zero)."""
+    assert m.Rates(220, 10000).samples_per_symbol == o.lib().or_rates_samples_per_symbol(220, 10000)
+    with pytest.raises(m.ModemPanic):
+        m.Rates(0, 10000)
+
+
+def test_carrier_host_phase(m, o):
+    """carrier.rs:17-26 on the host entry point, bit-exact vs the oracle."""
+    w = m.Freq(1000, 10000).sample_freq()
+    c = m.Carrier(m.Freq(1000, 10000))
+    for s0 in (0, (1 << 24) - 3, (1 << 26) + 5, (1 << 33) + 1):
+        want = o.carrier_phases(w, s0, 4)
+        got = np.array([c.inner(s0 + k) for k in range(4)], np.float32)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    c.sample = 7
+    assert c.next() == c.inner(7) and c.sample == 8
+
+
+def product_and_oracle_phasors(m, o):
+    rings = [(0, 4, 0.5, float(np.float32(np.pi / 4))), (4, 16, 1.0, float(np.float32(np.pi / 12)))]
+    return [
+        (m.BPSK(PI_4, 1.0), o.new_phasor(o.BPSK, PI_4, 1.0)),
+        (m.BPSK(0.3, 2.5), o.new_phasor(o.BPSK, 0.3, 2.5)),
+        (m.QPSK(0.0, 1.0), o.new_phasor(o.QPSK, 0.0, 1.0)),
+        (m.QPSK(0.7, 0.5), o.new_phasor(o.QPSK, 0.7, 0.5)),
+        (m.QAM(4, 0.0, 1.0), o.new_phasor(o.QAM, 4, 0.0, 1.0)),
+        (m.QAM(8, 0.0, 1.0), o.new_phasor(o.QAM, 8, 0.0, 1.0)),
+        (m.QAM(6, 0.2, 3.0), o.new_phasor(o.QAM, 6, 0.2, 3.0)),
+        (m.BASK(1.0), o.new_phasor(o.BASK, 1.0)),
+        (m.MPSK(4, 0.0, 1.0), o.new_phasor(o.MPSK, 4, 0.0, 1.0)),
+        (m.MPSK(3, 0.1, 2.0), o.new_phasor(o.MPSK, 3, 0.1, 2.0)),
+        (m.OQPSK(1.0), o.new_phasor(o.OQPSK, 1.0)),
+        (m.APSK(1.0, 4, [m.Ring(range(a, b), r, ph) for a, b, r, ph in rings]),
+         o.new_phasor(o.APSK, 1.0, 4, rings)),
+    ]
+
+
+def test_phasor_luts_bit_exact(m, o):
+    """The host-built (I, Q) table equals the reference phasor's i/q for every bit pattern."""
+    for prod, orc in product_and_oracle_phasors(m, o):
+        got, want = prod.lut(), o.phasor_lut(orc)
+        assert prod.bits_per_symbol() == orc.bits_per_symbol
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), type(prod).__name__
+
+
+def test_phasor_methods_mirror_reference(m, o):
+    """DigitalPhasor::i/q/next (phasor.rs:1-12) on explicit bit slices."""
+    q = m.QAM(4, 0.0, 6.0)                               # qam.rs:68-84 through the product
+    assert (q.i(0, [1, 0, 1, 1]), q.q(0, [1, 0, 1, 1])) == (1.0, 3.0)
+    assert q.next(0, [0, 0, 0, 1]) == (-3.0, -1.0)
+
+
+def test_phasor_panics(m):
+    """assert!s of the reference become ModemPanic (qam.rs:17, apsk.rs:26/74)."""
+    with pytest.raises(m.ModemPanic):
+        m.QAM(1, 0.0, 1.0).lut()
+    with pytest.raises(m.ModemPanic):
+        m.Ring(range(0, 4), 1.5, 0.0)
+    with pytest.raises(m.ModemPanic):                    # rings do not cover 0..2^bps
+        m.APSK(1.0, 4, [m.Ring(range(0, 4), 0.5, 0.0)])
+
+
+def test_slicer_desc(m, o):
+    """QAM phase 0 -> the per-axis slicer with the oracle's constants; others -> nearest LUT."""
+    d = m.QAM(4, 0.0, 1.0).slicer()
+    s = o.qam_axis_slicer(4, 1.0)
+    assert d.kind == m.SLICER_QAM_AXIS
+    assert np.float32(d.inv_scale) == np.float32(s.inv_scale)
+    assert np.float32(d.max_symbol) == np.float32(s.max_symbol)
+    assert m.QPSK(0.0, 1.0).slicer().kind == m.SLICER_NEAREST
+
+
+@pytest.mark.parametrize("L,sps", [(33, 4), (65, 4), (129, 4), (513, 8)])
+def test_rrc_taps_match_oracle(m, o, L, sps):
+    assert np.array_equal(m.rrc_taps(L, sps, 0.35).view(np.uint32), o.rrc_taps(L, sps, 0.35).view(np.uint32))
+
+
+def test_rrc_taps_invalid(m):
+    with pytest.raises(m.ModemPanic):
+        m.rrc_taps(0, 4, 0.35)
+
+
+# ----------------------------------------------- device entry points without a device ----
+def _no_gpu():
+    import torch
+    return not torch.cuda.is_available()
+
+
+@pytest.mark.skipif(not _no_gpu(), reason="checks the no-device path")
+def test_device_calls_fail_with_status(m):
+    taps = m.rrc_taps(33, 4, 0.35)
+    with pytest.raises(m.ModemError) as e:
+        m.DigitalModulator(m.Carrier(m.Freq(1, 4)), m.QPSK(0.0, 1.0), 4, taps)
+    assert e.value.status in (m.ERR_NO_DEVICE, m.ERR_HIP)
+    with pytest.raises(m.ModemError) as e:
+        m.DemodulatorRx(m.Carrier(m.Freq(1, 4)), taps, decim=4, decim_offset=32)
+    assert e.value.status in (m.ERR_NO_DEVICE, m.ERR_HIP)
+    with pytest.raises(m.ModemError):
+        m.FIRFilter(taps)
+
+
+def test_null_and_bad_arguments(m):
+    """Raw C ABI: NULL / out-of-range arguments return INVALID_ARG instead of crashing."""
+    L = m.load_library()
+    lib = ctypes.CDLL(m.lib_path())
+    lib.modem_tx_create.restype = ctypes.c_int
+    lib.modem_tx_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    assert lib.modem_tx_create(None, 0, None) == m.ERR_INVALID_ARG
+    lib.modem_rx_create.restype = ctypes.c_int
+    lib.modem_rx_create.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    assert lib.modem_rx_create(None, 0, None) == m.ERR_INVALID_ARG
+    lib.modem_tx_destroy.restype = ctypes.c_int
+    lib.modem_tx_destroy.argtypes = [ctypes.c_void_p]
+    assert lib.modem_tx_destroy(None) == m.MODEM_OK          # like free(NULL)
+    lib.modem_rates_sps.restype = ctypes.c_int
+    lib.modem_rates_sps.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+    sps = ctypes.c_uint64()
+    assert lib.modem_rates_sps(0, 10000, ctypes.byref(sps)) == m.ERR_INVALID_ARG
+    assert lib.modem_rates_sps(220, 10000, ctypes.byref(sps)) == m.MODEM_OK and sps.value == 45
+    assert L is not None
+
+
+def test_product_luts_match_fixtures(m):
+    """The host-built tables equal the committed LUT fixtures (tests/golden/luts.npz)."""
+    with np.load(os.path.join(ROOT, "tests", "golden", "luts.npz")) as z:
+        for key, ph in (("bpsk_pi4", m.BPSK(PI_4, 1.0)), ("qpsk", m.QPSK(0.0, 1.0)),
+                        ("qam16", m.QAM(4, 0.0, 1.0)), ("qam256", m.QAM(8, 0.0, 1.0))):
+            assert np.array_equal(ph.lut().view(np.uint32), z[key].view(np.uint32)), key

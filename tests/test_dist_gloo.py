@@ -1,0 +1,98 @@
+"""bench.py's multi-rank harness with world_size 2 over gloo on the CPU.
+
+Channels shard across ranks with no data-path collective: each rank runs its own channel set,
+the only communication is the timing barrier and the max-over-ranks reduction. The GPU runner
+is replaced by a small CPU runner built on the oracle (test infrastructure), so the test covers
+the harness arithmetic and the rank → channel assignment, not the kernels.
+"""
+import json
+import os
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class CpuRunner:
+    """Oracle TX -> RX on a tiny channel per rank (stand-in for bench.GpuRunner)."""
+
+    def __init__(self, wl, rank, o, bench):
+        name, bps, L, sps, nsamp, nch, dtype, _ = wl
+        self.o, self.rank, self.bps, self.L, self.sps = o, rank, bps, L, sps
+        self.p = o.new_phasor(o.QAM, bps, 0.0, 1.0)
+        self.taps = o.rrc_taps(L, sps, 0.35)
+        self.w = o.sample_freq(1, 4)
+        self.seeds = [bench.channel_seed(rank, nch, c) for c in range(nch)]
+        self.bits = [o.prng_bits(s, nsamp // sps * bps) for s in self.seeds]
+        self.steps = 0
+
+    def step(self):
+        o = self.o
+        self.out = []
+        for b in self.bits:
+            y = o.tx_chain(self.p, b, self.sps, self.taps, self.w, 0)
+            self.out.append(o.rx_chain(y, self.w, 0, o.MIX_COMPLEX, self.taps, self.sps, self.L - 1,
+                                       o.qam_axis_slicer(self.bps, 1.0))[1])
+        if self.rank == 1:
+            time.sleep(0.05)                 # the slower rank sets the reported time
+        self.steps += 1
+
+    def sync(self):
+        pass
+
+    def kernel_times_ms(self, reps):
+        return 0.01, 0.02
+
+    def check(self):
+        sent = self.bits[0].reshape(-1, self.bps).astype(np.int64) @ (1 << np.arange(self.bps)[::-1])
+        return bool(np.array_equal(self.out[0], sent[: len(self.out[0])].astype(np.uint8)))
+
+
+def _worker(rank, world, port, outdir):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as td
+    import bench
+    import oracle as o
+    td.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    bench.WORKLOADS["tiny"] = ("qam16", 4, 129, 4, 1 << 12, 2, 0, "tiny: 2 channels x 4096 samples")
+    args = bench.argparse.Namespace(config="tiny", steps=3, warmup=1, no_cpu_baseline=True, cpu_samples=0)
+    runners = []
+
+    def factory(wl, r):
+        runners.append(CpuRunner(wl, r, o, bench))
+        return runners[0]
+
+    out = bench.run(args, factory, bench._Dist(td, None), rank, world)
+    out["_seeds"] = runners[0].seeds
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump(out, f)
+    td.destroy_process_group()
+
+
+def test_two_ranks_gloo(tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    outs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    for out in outs:
+        assert out["n_gpus"] == world and out["scaling"] == "weak"
+        assert out["decisions_match_sent"] is True
+        assert "cpu_baseline" not in out               # only rank 0 at N = 1 times the CPU
+    # both ranks report the same (max-over-ranks) time and the whole-job sample count
+    assert outs[0]["ms_per_step"] == outs[1]["ms_per_step"]
+    assert outs[0]["ms_per_step"] >= 50.0              # rank 1 sleeps 50 ms per step
+    total = (1 << 12) * 2 * 3 * world
+    assert abs(outs[0]["value"] - total / (outs[0]["ms_per_step"] * 3 / 1e3) / 1e6) <= 0.02 * outs[0]["value"]
+    # ranks own disjoint channels
+    assert not set(outs[0]["_seeds"]) & set(outs[1]["_seeds"])
