@@ -269,7 +269,7 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--cpu-samples", type=int, default=1 << 23)
+    ap.add_argument("--cpu-samples", type=int, default=1 << 25)   # ~15 s of oracle work
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
