@@ -1,0 +1,235 @@
+// rust-modem_amd/csrc/modem_device.h — device helpers shared by the gfx950 kernel files
+// (modem_tx.hip, modem_rx.hip, modem_misc.hip): the bit-exact carrier phase, sin/cos, vector
+// helpers, sample I/O and the persistent-grid sizing used by every launcher.
+#pragma once
+#include "modem_internal.h"
+
+#include <hip/hip_fp16.h>
+
+#include <map>
+#include <mutex>
+#include <utility>
+
+namespace mk {
+
+// ----------------------------------------------------------------------------------------
+// Bit-exact reference carrier phase: mod_trig(w * (n as f32)).
+//   x = fl(w * fl(n)); phase = fl(x - fl(TWO_PI * floor(fl(x / TWO_PI)))).
+// fl(x / TWO_PI) is replaced by q1 = q0 + r*RC (q0 = x*RC, r = fma(-q0, TWO_PI, x)):
+// q1 differs from the IEEE quotient for some x but floor(q1) == floor(fl(x/TWO_PI)) for
+// every non-negative finite f32 (checked exhaustively on the host: tests/test_phase_math.py),
+// so the phase is bit-identical. contract(off) keeps TWO_PI*f and the subtraction
+// separately rounded, as rustc does.
+constexpr float kTwoPi = 0x1.921fb6p+2f;   // std::f32::consts::PI * 2.0 (0x40c90fdb)
+constexpr float kRcp2Pi = 0x1.45f306p-3f;  // fl(1 / kTwoPi)
+
+__device__ __forceinline__ float phase_from_f(float w, float nf) {
+#pragma clang fp contract(off)
+    const float x = w * nf;
+    const float q0 = x * kRcp2Pi;
+    const float r = __builtin_fmaf(-q0, kTwoPi, x);
+    const float q1 = __builtin_fmaf(r, kRcp2Pi, q0);
+    const float f = __builtin_floorf(q1);
+    const float p = kTwoPi * f;
+    return x - p;
+}
+
+// `n as f32` with round-to-nearest-even: one v_cvt_f32_u32 below 2^32, the compiler's
+// exact u64 -> f32 sequence above.
+__device__ __forceinline__ float carrier_phase(float w, uint64_t n, bool small_n) {
+    const float nf = small_n ? (float)(uint32_t)n : (float)n;
+    return phase_from_f(w, nf);
+}
+
+// Same, for n = base + off with a wave-uniform 64-bit base and a 32-bit lane offset.
+__device__ __forceinline__ float carrier_phase_off(float w, uint64_t base, int off, bool small_n) {
+    const float nf = small_n ? (float)((uint32_t)base + (uint32_t)off) : (float)(base + (int64_t)off);
+    return phase_from_f(w, nf);
+}
+
+// sin/cos of a phase in [0, 2pi]. MODEM_PRECISE_TRIG selects a Cody-Waite + minimax
+// polynomial (<= 2 ulp); the default uses the hardware v_sin_f32/v_cos_f32 (input in
+// revolutions). Either way the sample tolerance is set in tests/test_gpu_parity.py.
+__device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
+#if defined(MODEM_ABLATE_TRIG)        // profiling builds only (tools/ablate.sh)
+    s = ph; c = 1.0f;
+    return;
+#endif
+#ifdef MODEM_PRECISE_TRIG
+    const float j = __builtin_rintf(ph * 0.63661977236758134f);
+    float r = __builtin_fmaf(-j, 1.57079637050628662f, ph);
+    r = __builtin_fmaf(-j, -4.37113900018624283e-8f, r);
+    const float r2 = r * r;
+    float sp = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+    sp = __builtin_fmaf(r2, sp, -1.6666654611e-1f);
+    const float sr = __builtin_fmaf(r * r2, sp, r);
+    float cp = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    cp = __builtin_fmaf(r2, cp, 4.166664568298827e-2f);
+    const float cr = __builtin_fmaf(r2 * r2, cp, __builtin_fmaf(-0.5f, r2, 1.0f));
+    const int q = (int)j & 3;
+    const float ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+    s = (q & 2) ? -ss : ss;
+    c = ((q + 1) & 2) ? -cc : cc;
+#else
+    s = __sinf(ph);
+    c = __cosf(ph);
+#endif
+}
+
+typedef const __attribute__((address_space(4))) float cfloat;   // wave-uniform -> s_load
+// (re, im) pair: one v_pk_fma_f32 per complex x real MAC, tap broadcast from an SGPR.
+typedef float cf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ cf2 ldc(const float2* p) { return *reinterpret_cast<const cf2*>(p); }
+__device__ __forceinline__ cf2 cmac(cf2 x, float h, cf2 acc) {
+    return __builtin_elementwise_fma(x, (cf2){h, h}, acc);
+}
+
+
+template <typename OutT> struct OutIO;
+template <> struct OutIO<float> {
+    __device__ static void store_pair(void* out, int64_t j, float a, float b, float c, float d) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + 2 * j) = make_float4(a, b, c, d);
+    }
+    __device__ static void store_one(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + 2 * j) = make_float2(a, b);
+    }
+    __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + j) = make_float2(a, b);
+    }
+    __device__ static void store_real_one(void* out, int64_t j, float a) {
+        reinterpret_cast<float*>(out)[j] = a;
+    }
+};
+template <> struct OutIO<__half> {
+    __device__ static void store_pair(void* out, int64_t j, float a, float b, float c, float d) {
+        const __half2 h0 = __floats2half2_rn(a, b), h1 = __floats2half2_rn(c, d);
+        uint2 u;
+        u.x = *reinterpret_cast<const uint32_t*>(&h0);
+        u.y = *reinterpret_cast<const uint32_t*>(&h1);
+        *reinterpret_cast<uint2*>(reinterpret_cast<__half*>(out) + 2 * j) = u;
+    }
+    __device__ static void store_one(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + 2 * j) = __floats2half2_rn(a, b);
+    }
+    __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
+        *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + j) = __floats2half2_rn(a, b);
+    }
+    __device__ static void store_real_one(void* out, int64_t j, float a) {
+        reinterpret_cast<__half*>(out)[j] = __float2half_rn(a);
+    }
+};
+
+enum { OUT_IQ_MIXED = 0, OUT_IQ_BASEBAND = 1, OUT_REAL = 2 };
+
+
+// Sliding register window: win[0] <- v, the rest shift up.
+template <int R>
+__device__ __forceinline__ void shift_in(cf2 (&win)[R], cf2 v) {
+#pragma unroll
+    for (int r = R - 1; r > 0; --r) win[r] = win[r - 1];
+    win[0] = v;
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Keep a loaded value in its register: an opaque asm use stops the compiler from
+// rematerialising the load inside a tile loop (where its vmcnt wait would also drain the
+// next tile's prefetch, since vector-memory counters retire in issue order).
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+
+// ---------------------------------------------------------------------- dispatch ----
+// Persistent grids: resident workgroups per CU (occupancy API, cached per kernel and LDS
+// size) x CUs, never more than the number of tiles.
+static inline int device_cus() {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
+static std::mutex g_occ_mu;
+static std::map<std::pair<const void*, size_t>, int> g_occ;
+
+static inline int resident_blocks(const void* kernel, int threads, size_t lds) {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto key = std::make_pair(kernel, lds);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) return it->second;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, threads, lds) != hipSuccess || occ <= 0) {
+        (void)hipGetLastError();
+        occ = 1;
+    }
+    g_occ[key] = occ;
+    return occ;
+}
+
+static inline unsigned persistent_grid(const void* kernel, int threads, size_t lds, int64_t ntiles) {
+    const int64_t cap = (int64_t)resident_blocks(kernel, threads, lds) * device_cus();
+    const int64_t g = ntiles < cap ? ntiles : cap;
+    return (unsigned)(g > 0 ? g : 1);
+}
+
+
+// acc_re/acc_im += sum_s A_s * B_s over NKS k-steps; A_s (complex) is read from LDS at
+// arow[off(s)], PD k-steps ahead of its MFMA pair (explicit software pipeline: the
+// scheduling barriers keep the compiler from collapsing it to one read of look-ahead).
+template <int NKS, int PD, typename OffF>
+__device__ __forceinline__ void mfma_chain(const float2* arow, OffF off, const float (&bf)[NKS],
+                                           f32x4& dre, f32x4& dim) {
+#ifdef MODEM_ABLATE_FIR
+    const float2 a0 = arow[off(0)];
+    dre[0] += a0.x * bf[0]; dim[0] += a0.y * bf[NKS - 1];
+    return;
+#endif
+    float2 a[PD];
+#pragma unroll
+    for (int s = 0; s < PD && s < NKS; ++s) a[s] = arow[off(s)];
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const float2 cur = a[s % PD];
+        if (s + PD < NKS) a[s % PD] = arow[off(s + PD)];
+        dre = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.x, bf[s], dre, 0, 0, 0);
+        dim = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.y, bf[s], dim, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// The same chain with B also read from LDS, at brow[4*s] (a Toeplitz band table: one
+// conflict-free ds_read_b32 per k-step instead of NKS fragment registers per lane).
+template <int NKS, int PD, typename OffF>
+__device__ __forceinline__ void mfma_chain_lb(const float2* arow, OffF off, const float* brow,
+                                              f32x4& dre, f32x4& dim) {
+#ifdef MODEM_ABLATE_FIR
+    const float2 a0 = arow[off(0)];
+    dre[0] += a0.x * brow[0]; dim[0] += a0.y * brow[4];
+    return;
+#endif
+    float2 a[PD];
+    float b[PD];
+#pragma unroll
+    for (int s = 0; s < PD && s < NKS; ++s) {
+        a[s] = arow[off(s)];
+        b[s] = brow[4 * s];
+    }
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        const float2 cur = a[s % PD];
+        const float cb = b[s % PD];
+        if (s + PD < NKS) {
+            a[s % PD] = arow[off(s + PD)];
+            b[s % PD] = brow[4 * (s + PD)];
+        }
+        dre = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.x, cb, dre, 0, 0, 0);
+        dim = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.y, cb, dim, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+
+}  // namespace mk
