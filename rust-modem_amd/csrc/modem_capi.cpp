@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -463,7 +464,8 @@ struct modem_rx {
     int64_t consumed = 0;          // stream samples processed
     modem_slicer_desc slicer{};
     int mfma_ksteps = 0;            // > 0: matched filter on the matrix pipe (rx_mfma)
-    float* d_bfrag = nullptr;       // its reversed-tap band table (rx_mfma_table_len floats)
+    float* d_bfrag = nullptr;       // its split-f16 tap tables (modem_internal.h)
+    int tap_scale_exp = 0;          // the tables hold h * 2^tap_scale_exp
     float* d_taps = nullptr;
     float2* d_slut = nullptr;
     void* d_hist[2] = {nullptr, nullptr};
@@ -538,17 +540,29 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
     const bool force_valu = env && std::strcmp(env, "valu") == 0;
     h->mfma_ksteps = force_valu ? 0 : mk::rx_mfma_ksteps((int)h->decim, (int)h->ntaps);
     if (h->mfma_ksteps > 0) {
-        // B[w][c] = h[W - 1 - w - (15 - c)*decim] is a Toeplitz band: lane (g, c) at k-step s
-        // (w = 4s + g) reads T[4s + g + (15 - c)*decim] of the reversed, zero-padded taps
-        // T[j] = h[W - 1 - j] (rx_mfma stages T in LDS; modem_kernels.hip).
-        const int nks = h->mfma_ksteps, W = 4 * nks, dec = (int)h->decim;
-        std::vector<float> bf((size_t)mk::rx_mfma_table_len(dec, nks), 0.0f);
-        for (int j = 0; j < W + 15 * dec; ++j) {
-            const int u = W - 1 - j;
-            if (u >= 0 && u < (int)h->ntaps) bf[(size_t)j] = d->taps[u];
-        }
-        if ((st = dalloc(&h->d_bfrag, bf.size()))) { delete h; return st; }
-        if (hipMemcpy(h->d_bfrag, bf.data(), bf.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        // Split-f16 tap tables of rx_mfma (modem_rx.hip): the reversed taps T[x] = h[W-1-x]
+        // scaled by 2^kb (max |h| * 2^kb in [2^14, 2^15): exact, keeps f16 in range), as f16
+        // hi then lo = rn_f16(v - hi), in NC copies shifted by gcd(decim, 8) so that every
+        // lane's 8-tap read is 16-B aligned.
+        const int nks = h->mfma_ksteps, W = 32 * nks, dec = (int)h->decim;
+        const int nc = mk::rx_mfma_table_copies(dec), tb = mk::rx_mfma_table_len(dec, nks), gq = 8 / nc;
+        float hmax = 0.0f;
+        for (uint32_t k = 0; k < h->ntaps; ++k) hmax = std::max(hmax, std::fabs(d->taps[k]));
+        int kb = 0;
+        if (hmax > 0.0f && std::isfinite(hmax)) { int e; std::frexp(hmax, &e); kb = 15 - e; }
+        h->tap_scale_exp = kb;
+        std::vector<_Float16> tab((size_t)nc * 2 * tb, (_Float16)0.0f);
+        for (int c = 0; c < nc; ++c)
+            for (int y = 0; y < tb; ++y) {
+                const int u = W - 1 - (y + c * gq);
+                const float v = (u >= 0 && u < (int)h->ntaps) ? std::ldexp(d->taps[u], kb) : 0.0f;
+                const _Float16 hi = (_Float16)v;
+                tab[((size_t)c * 2) * tb + y] = hi;
+                tab[((size_t)c * 2 + 1) * tb + y] = (_Float16)(v - (float)hi);
+            }
+        const size_t nfl = (tab.size() * sizeof(_Float16) + sizeof(float) - 1) / sizeof(float);
+        if ((st = dalloc(&h->d_bfrag, nfl))) { delete h; return st; }
+        if (hipMemcpy(h->d_bfrag, tab.data(), tab.size() * sizeof(_Float16), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
         }
     }
@@ -620,6 +634,7 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
     p.inv_scale = h->slicer.inv_scale;
     p.max_symbol = h->slicer.max_symbol;
     p.w = h->w;
+    p.tap_scale_exp = h->tap_scale_exp;
     if (h->mfma_ksteps > 0)
         HIP_TRY(mk::launch_rx_mfma(p, (int)h->decim, h->mfma_ksteps, h->d_bfrag, h->in_dtype, h->out_dtype,
                                    h->mix, s));

@@ -59,6 +59,7 @@ struct RxParams {
     float inv_scale;
     float max_symbol;
     float w;
+    int32_t tap_scale_exp;   // rx_mfma: tables hold h * 2^tap_scale_exp
 };
 
 struct FirParams {
@@ -79,11 +80,17 @@ hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStr
 int tx_mfma_ksteps(int sps, int K);
 hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const float* bfrag, int dtype,
                           int out_mode, hipStream_t s);
-// RX matched filter on the matrix pipe (rx_mfma): ksteps for (decim, ntaps) or 0.
+// RX matched filter on the matrix cores (rx_mfma, split-f16 MFMA): 32-sample k-steps for
+// (decim, ntaps), or 0 when no variant fits.
 int rx_mfma_ksteps(int decim, int L);
-// Floats in its band table T[j] = h[W - 1 - j], j < 4*nks + 15*decim (rounded up to 4).
-constexpr int rx_mfma_table_len(int decim, int nks) { return (4 * nks + 15 * decim + 3) & ~3; }
-hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const float* bfrag, int in_dtype,
+// Its tap tables: rx_mfma_table_copies(decim) copies q of the reversed taps
+// T[x] = h[W - 1 - x] * 2^tap_scale_exp (W = 32*nks), copy q holding T[y + q*gcd(decim, 8)],
+// each as hi then lo f16 halves of rx_mfma_table_len(decim, nks) entries.
+constexpr int rx_mfma_table_copies(int decim) {
+    return 8 / (decim % 8 == 0 ? 8 : decim % 4 == 0 ? 4 : decim % 2 == 0 ? 2 : 1);
+}
+constexpr int rx_mfma_table_len(int decim, int nks) { return (32 * nks + 15 * decim + 8 + 7) & ~7; }
+hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const void* tables, int in_dtype,
                           int out_dtype, int mix, hipStream_t s);
 hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,
                      hipStream_t s);

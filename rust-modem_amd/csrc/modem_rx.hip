@@ -296,21 +296,28 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
 }
 
 // ----------------------------------------------------------------------- RX on MFMA ----
-// Matched filter at the kept instants as f32 matrix products (v_mfma_f32_16x16x4_f32):
+// Matched filter at the kept instants on the matrix cores (v_mfma_f32_16x16x32_f16):
 //   rows i = 16 groups of 16 consecutive kept instants, cols c = instant in the group,
-//   k = w  = offset in a W = 4*NKS sample window ending at the group's last instant,
-//   A[i][w] = z[start_i + w]  (mixed input from LDS; one chain for re, one for im),
-//   B[w][c] = h[W - 1 - w - (15 - c)*DEC]  (banded tap matrix: NKS VGPRs per lane).
-// MAC efficiency = L / W (0.67 for 129 taps at decimation 4). One wave: one 16x16 tile
-// (256 instants) per 2*NKS MFMAs. LDS keeps the mixed samples in natural order with 2 pad
-// samples after every RW = 16*DEC (one row of A), so the 16 rows of a read land in distinct
-// banks and every k-step is a compile-time immediate offset.
+//   k = w = offset in a W = 32*NKS sample window ending at the group's last instant,
+//   A[i][w] = z[start_i + w] (mixed input), B[w][c] = h[W - 1 - w - (15 - c)*DEC].
+// Every real operand is split in two f16 halves, a = a_hi + a_lo (round to nearest), and
+//   A*B ~= A_hi*B_hi + A_hi*B_lo + A_lo*B_hi      (dropped A_lo*B_lo < 2^-22 |a||b|)
+// accumulates in f32: 6 MFMAs (re and im rails) per 32-sample k-step, 16x the MAC rate of
+// the f32 MFMA. Range: the taps are scaled by 2^kb on the host (max in [2^14, 2^15)); the
+// mixed samples of a tile are used as they are when the tile's max |z| lies in
+// [2^-3, 2^15) (results then never depend on how a stream is cut into calls), and scaled
+// by 2^ka into [2^14, 2^15) otherwise. Outputs are scaled back with ldexp (exact).
+// LDS: four f16 planes (re_hi, re_lo, im_hi, im_lo) in natural sample order with 8 pad
+// halves after every RW = 16*DEC samples (the 16 rows of a 16-B read hit distinct bank
+// groups), and NC shifted copies of the hi/lo reversed-tap table so that every lane's
+// 8-tap B read is one aligned ds_read_b128.
 template <int DEC> struct RxMfmaCfg {
     static constexpr int NT = 256;               // 4 waves
     static constexpr int TS = 4 * 256;           // kept instants per workgroup tile
     static constexpr int RW = 16 * DEC;          // samples per A row
+    static constexpr int RP = RW + 8;            // padded row pitch (halves)
 };
-__host__ __device__ constexpr int rxm_pos(int e, int RW) { return e + 2 * (e / RW); }
+__host__ __device__ constexpr int rxh_pos(int e, int RW) { return e + 8 * (e / RW); }
 
 // What the steady-state epilogue writes: baseband IQ, QAM-axis decisions, or both
 // (RXE_GEN: any other combination, guarded per store).
@@ -327,82 +334,214 @@ __device__ __forceinline__ uint8_t rx_slice_qam(const RxParams& p, float re, flo
     return (uint8_t)((si << p.bits_per_carrier) | sq);
 }
 
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+// hi = rn_f16(v), lo = rn_f16(v - hi) for two values (v - hi is exact in f32).
+__device__ __forceinline__ void split2(cf2 v, h2& hi, h2& lo) {
+    hi = __builtin_convertvector(v, h2);
+    lo = __builtin_convertvector(v - __builtin_convertvector(hi, cf2), h2);
+}
+
+// Four consecutive input samples (one lane's staging quad).
+template <typename InT> struct Quad;
+template <> struct Quad<float> {
+    struct T { float4 a, b; };
+    __device__ static T load(const void* x, int64_t q) {      // q: sample index (8-B aligned)
+        const float4* v = reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(x) + q);
+        return T{v[0], v[1]};
+    }
+    __device__ static void split(const T& t, float2 (&x)[4]) {
+        x[0] = make_float2(t.a.x, t.a.y); x[1] = make_float2(t.a.z, t.a.w);
+        x[2] = make_float2(t.b.x, t.b.y); x[3] = make_float2(t.b.z, t.b.w);
+    }
+};
+template <> struct Quad<__half> {
+    using T = uint4;
+    __device__ static T load(const void* x, int64_t q) {
+        return *reinterpret_cast<const uint4*>(reinterpret_cast<const __half2*>(x) + q);
+    }
+    __device__ static void split(const T& t, float2 (&x)[4]) {
+        x[0] = __half22float2(*reinterpret_cast<const __half2*>(&t.x));
+        x[1] = __half22float2(*reinterpret_cast<const __half2*>(&t.y));
+        x[2] = __half22float2(*reinterpret_cast<const __half2*>(&t.z));
+        x[3] = __half22float2(*reinterpret_cast<const __half2*>(&t.w));
+    }
+};
+
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, off));
+    return m;
+}
+
+// Tile scale exponent from the lanes' max |z| (one barrier; red: 4 floats of LDS).
+__device__ __forceinline__ int tile_scale_exp(float lane_max, float* red) {
+    const float wm = wave_max(lane_max);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
+    __syncthreads();
+    const float m = __builtin_fmaxf(__builtin_fmaxf(red[0], red[1]), __builtin_fmaxf(red[2], red[3]));
+    const int ex = (int)((__float_as_uint(m) >> 23) & 0xff);
+    if (ex >= 127 - 3 && ex < 127 + 15) return 0;          // max in [2^-3, 2^15): as is
+    if (ex == 0 || ex == 0xff) return 0;                    // all zero / non-finite
+    return 141 - ex;                                        // max * 2^k in [2^14, 2^15)
+}
+
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
 struct RxMfma {
     using C = RxMfmaCfg<DEC>;
-    using IO = InIO<InT>;
-    using Raw = typename IO::Raw;
-    static constexpr int NT = C::NT, TS = C::TS, RW = C::RW;
-    static constexpr int W = 4 * NKS;
-    static constexpr int NS = (TS - 16) * DEC + W;            // samples staged per tile
-    static constexpr int U = (NS + 1 + 2 * NT - 1) / (2 * NT); // prefetched sample pairs per lane
+    using Q = Quad<InT>;
+    using QT = typename Q::T;
+    static constexpr int NT = C::NT, TS = C::TS, RW = C::RW, RP = C::RP;
+    static constexpr int W = 32 * NKS;
+    static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
+    static constexpr int NQ = (NS + 3) / 4;                     // quads
+    static constexpr int U = (NQ + NT - 1) / NT;                // quads per lane
+    static constexpr int PL = (rxh_pos(4 * NQ - 1, RW) + 1 + 7) & ~7;   // halves per plane
+    static constexpr int NC = rx_mfma_table_copies(DEC);
+    static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
+    static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 16;
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
 
-    // Tile t stages chunk samples q_lo .. q_lo + NS - 1 (window start of its first row).
+    // Rows hold 16 instants aligned to the absolute instant index (k % 16 == column), so an
+    // instant's taps always fall at the same k positions of the 32-wide MFMA sums and the
+    // result never depends on where a call starts. Tile t covers instants
+    // kb + t*TS .., kb = k_first - lead; outputs before k_first are computed and dropped.
+    __device__ static int lead(const RxParams& p) { return (int)(p.k_first & 15); }
     __device__ static int64_t q_lo_of(const RxParams& p, int64_t t) {
-        return (p.k_first + t * TS) * DEC + p.D + 15 * DEC - W + 1 - p.n_start;
+        return (p.k_first - lead(p) + t * TS) * DEC + p.D + 15 * DEC - W + 1 - p.n_start;
     }
 
-    // Steady state: the tile's samples are whole pairs of this chunk, carrier index < 2^32,
-    // every instant is kept. PAR = q_lo & 1 is the same for every tile of a call (TS*DEC even).
-    template <int PAR>
-    __device__ static void stage_fast(const RxParams& p, float2* lds, uint32_t nb32, const Raw (&pre)[U]) {
+    // Scale, split and write samples e0..e0+3 (e0 % 4 == 0: one row, 8-B aligned).
+    __device__ static void put4(_Float16* pl, int e0, const float (&zr)[4], const float (&zi)[4], float sc) {
+        h2 rh0, rl0, rh1, rl1, ih0, il0, ih1, il1;
+        split2((cf2){zr[0], zr[1]} * sc, rh0, rl0);
+        split2((cf2){zr[2], zr[3]} * sc, rh1, rl1);
+        split2((cf2){zi[0], zi[1]} * sc, ih0, il0);
+        split2((cf2){zi[2], zi[3]} * sc, ih1, il1);
+        const int o = rxh_pos(e0, RW);
+        *reinterpret_cast<h4*>(pl + o) = (h4){rh0.x, rh0.y, rh1.x, rh1.y};
+        *reinterpret_cast<h4*>(pl + PL + o) = (h4){rl0.x, rl0.y, rl1.x, rl1.y};
+        *reinterpret_cast<h4*>(pl + 2 * PL + o) = (h4){ih0.x, ih0.y, ih1.x, ih1.y};
+        *reinterpret_cast<h4*>(pl + 3 * PL + o) = (h4){il0.x, il0.y, il1.x, il1.y};
+    }
+
+    // Steady state: the tile's samples lie inside the chunk, carrier index < 2^32. Staged
+    // at scale 1 (the tile max is tracked on the way); a tile whose max falls outside
+    // [2^-3, 2^15) is restaged scaled by stage_slow. Returns the tile's scale exponent ka.
+    __device__ static int stage_fast(const RxParams& p, _Float16* pl, float* red, uint32_t nb32,
+                                     const QT (&pre)[U], int64_t q_lo) {
         const int tid = threadIdx.x;
+        // carrier index of the lane's first sample; opaque, so that the per-sample offsets
+        // stay immediates instead of 4*U hoisted loop-invariant VGPRs
+        uint32_t lb = nb32 + 4u * (uint32_t)tid;
+        asm volatile("" : "+v"(lb));
+        float mx = 0.f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            float2 x[2];
-            IO::split(pre[u], x[0], x[1]);
-            const int e0 = 2 * (tid + NT * u) - PAR;     // stage index of x[0]
-            float2 z[2];
+            float2 x[4];
+            Q::split(pre[u], x);
+            const int e0 = 4 * (tid + NT * u);
+            float zr[4], zi[4];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < 4; ++j) {
                 float sn, cs;
 #ifdef MODEM_ABLATE_MIX
-                sn = 0.f; cs = (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j));
+                sn = 0.f; cs = (float)(lb + (uint32_t)(4 * NT * u + j));
 #else
-                sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)(2 * (tid + NT * u) + j))), sn, cs);
+                sincos_phase(phase_from_f(p.w, (float)(lb + (uint32_t)(4 * NT * u + j))), sn, cs);
 #endif
-                if (MIX == MIX_REFERENCE_REAL) z[j] = make_float2(x[j].x * cs, x[j].x * -sn);
-                else z[j] = make_float2(__builtin_fmaf(x[j].y, sn, x[j].x * cs),
-                                        __builtin_fmaf(-x[j].x, sn, x[j].y * cs));
+                if (MIX == MIX_REFERENCE_REAL) { zr[j] = x[j].x * cs; zi[j] = x[j].x * -sn; }
+                else {
+                    zr[j] = __builtin_fmaf(x[j].y, sn, x[j].x * cs);
+                    zi[j] = __builtin_fmaf(-x[j].x, sn, x[j].y * cs);
+                }
+                // only the last slot can reach past the tile: its extra samples are not counted
+                if ((u + 1) * 4 * NT <= NS || e0 + j < NS)
+                    mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(zr[j]), __builtin_fabsf(zi[j])));
             }
-            // Only the first and last slots can fall outside [0, NS): the other guards are
-            // compile-time true, so the slots' chains interleave without branches.
-            const bool last = (u + 1) * 2 * NT > NS - 1;
-            if (PAR == 0) {
-                if (!last || e0 < NS)   // a pair never straddles a padded row (RW even): one 16-B store
-                    *reinterpret_cast<float4*>(lds + rxm_pos(e0, RW)) = make_float4(z[0].x, z[0].y, z[1].x, z[1].y);
-            } else {
-                if ((u > 0 || e0 >= 0) && (!last || e0 < NS)) lds[rxm_pos(e0, RW)] = z[0];
-                if (!last || e0 + 1 < NS) lds[rxm_pos(e0 + 1, RW)] = z[1];
-            }
+            if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, e0, zr, zi, 1.0f);
         }
+        const int ka = tile_scale_exp(mx, red);
+        if (ka != 0) {                                      // rare: out-of-window magnitudes
+            __syncthreads();                                // `red` is reused
+            return stage_slow(p, pl, red, q_lo);
+        }
+        return 0;
     }
 
-    // First / last tiles of a chunk, unaligned input, carrier index >= 2^32: per sample.
-    __device__ static void stage_slow(const RxParams& p, float2* lds, int64_t q_lo) {
+    // First / last tiles of a chunk, unaligned input, carrier index >= 2^32: per sample, two
+    // passes (max, then scale + split).
+    __device__ static int stage_slow(const RxParams& p, _Float16* pl, float* red, int64_t q_lo) {
         const int64_t n_lo = q_lo + p.n_start;
-        for (int e = threadIdx.x; e < NS; e += NT)
-            lds[rxm_pos(e, RW)] = rx_mix<MIX>(p, n_lo, e, rx_sample<InT>(p, q_lo + e));
+        float mx = 0.f;
+        for (int e0 = 4 * threadIdx.x; e0 < NS; e0 += 4 * NT)
+            for (int j = 0; j < 4 && e0 + j < NS; ++j) {
+                const float2 z = rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j));
+                mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(z.x), __builtin_fabsf(z.y)));
+            }
+        const int ka = tile_scale_exp(mx, red);
+        const float sc = __builtin_ldexpf(1.0f, ka < -126 ? -126 : (ka > 127 ? 127 : ka));
+        for (int e0 = 4 * threadIdx.x; e0 < NS; e0 += 4 * NT) {
+            float zr[4], zi[4];
+            for (int j = 0; j < 4; ++j) {
+                const float2 z = e0 + j < NS ? rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j))
+                                             : make_float2(0.f, 0.f);
+                zr[j] = z.x; zi[j] = z.y;
+            }
+            put4(pl, e0, zr, zi, sc);
+        }
+        return ka;
     }
 
-    static constexpr int TBL = rx_mfma_table_len(DEC, NKS);   // band table floats
-    static constexpr int LDS_SAMPLES = rxm_pos(NS, RW) + 2;      // float2 slots before the table
-
-    // One 16x16 tile per wave: instants kt + 16*i + c. Lane (g, c) reads A from row c of its
-    // wave's block and B[4s + g][c] = T[4s + g + (15 - c)*DEC] from the band table.
-    __device__ static void fir(const float2* lds, const float* tbl, f32x4& dre, f32x4& dim) {
+    // One 16x16 tile per wave. Lane (i = lane & 15, g = lane >> 4) reads A row i, samples
+    // 32s + 8g .. +7, and B[32s + 8g + j][c = i] = T[32s + 8g + j + (15 - c)*DEC].
+    __device__ static void fir(const _Float16* pl, const _Float16* tbl, f32x4& dre, f32x4& dim) {
         const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        const float2* arow = lds + rxm_pos(wave * 16 * RW, RW) + (lane & 15) * (RW + 2) + (lane >> 4);
-        const float* brow = tbl + (lane >> 4) + (15 - (lane & 15)) * DEC;
-        dre = (f32x4){0.f, 0.f, 0.f, 0.f};
-        dim = dre;
-        mfma_chain_lb<NKS, 4>(arow, [](int s) { return 4 * s + 2 * ((4 * s) / RW); }, brow, dre, dim);
+        const int i = lane & 15, g = lane >> 4;
+        const _Float16* arow = pl + (16 * wave + i) * RP + 8 * g;
+        const int xb = 8 * g + (15 - i) * DEC;                  // B start for this lane's column
+        const int q = xb & 7;                                   // copy with Tq[y] = T[y + q]
+        const _Float16* brow = tbl + (q / (8 / NC)) * 2 * TB + (xb - q);
+#ifdef MODEM_ABLATE_FIR
+        const h8 a0 = *reinterpret_cast<const h8*>(arow);
+        dre = (f32x4){(float)a0[0], 0.f, 0.f, 0.f};
+        dim = (f32x4){(float)brow[0], 0.f, 0.f, 0.f};
+        return;
+#endif
+        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0, m0 = r0, m1 = r0;
+        auto aoff = [](int s) { return 32 * s + 8 * ((32 * s) / RW); };
+        h8 a[2][4], b[2][2];
+        auto load = [&](int s, int slot) {
+            const int o = aoff(s);
+            a[slot][0] = *reinterpret_cast<const h8*>(arow + o);
+            a[slot][1] = *reinterpret_cast<const h8*>(arow + PL + o);
+            a[slot][2] = *reinterpret_cast<const h8*>(arow + 2 * PL + o);
+            a[slot][3] = *reinterpret_cast<const h8*>(arow + 3 * PL + o);
+            b[slot][0] = *reinterpret_cast<const h8*>(brow + 32 * s);
+            b[slot][1] = *reinterpret_cast<const h8*>(brow + TB + 32 * s);
+        };
+        load(0, 0);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const int c = s & 1;
+            if (s + 1 < NKS) load(s + 1, c ^ 1);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][0], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
+            r1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r1, 0, 0, 0);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][1], m1, 0, 0, 0);
+            r1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], b[c][0], r1, 0, 0, 0);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], b[c][0], m1, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        dre = r0 + r1;
+        dim = m0 + m1;
     }
 
     // D[row][col]: row = 4*(lane>>4) + r, col = lane&15 -> instant ot + 16*row + col.
     template <int EM>
-    __device__ static void emit_full(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim) {
+    __device__ static void emit_full(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
         const int lane = threadIdx.x & 63;
 #ifdef MODEM_ABLATE_STORE
 #pragma unroll
@@ -412,7 +551,7 @@ struct RxMfma {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
-            const float re = GAIN * dre[r], im = GAIN * dim[r];
+            const float re = GAIN * __builtin_ldexpf(dre[r], -kab), im = GAIN * __builtin_ldexpf(dim[r], -kab);
             if (EM == RXE_GEN) {
                 rx_emit<OutT>(p, ot + off, re, im);
                 continue;
@@ -422,40 +561,45 @@ struct RxMfma {
         }
     }
 
-    __device__ static void emit_edge(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim) {
+    __device__ static void emit_edge(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t o = ot + 16 * (4 * (lane >> 4) + r) + (lane & 15);
-            if (o < p.nout) rx_emit<OutT>(p, o, GAIN * dre[r], GAIN * dim[r]);
+            if (o >= 0 && o < p.nout)
+                rx_emit<OutT>(p, o, GAIN * __builtin_ldexpf(dre[r], -kab), GAIN * __builtin_ldexpf(dim[r], -kab));
         }
     }
 
-    // Tiles of [t0, t1). When the call's input is 16-B aligned and its carrier indices stay
-    // below 2^32, the run of "full" tiles (all staged samples inside the chunk, all 1024
-    // instants kept) goes through the prefetched loop, whose epilogue EM stores unconditionally;
-    // the first and last tiles of the chunk take the general path. PAR = q_lo & 1 is the same
-    // for every tile of a call (TS*DEC is even).
+    // Tiles of [t0, t1). When the input is 8-B aligned and the carrier indices stay below
+    // 2^32, the run of "full" tiles (all staged samples inside the chunk, all 1024 instants
+    // kept) goes through the prefetched loop, whose epilogue EM stores unconditionally; the
+    // first and last tiles of the chunk take the general path.
     template <int EM>
-    __device__ static void run(const RxParams& p, float2* lds, const float* bf, int64_t t0, int64_t t1) {
+    __device__ static void run(const RxParams& p, _Float16* pl, const _Float16* tbl, float* red,
+                               int64_t t0, int64_t t1) {
         const int tid = threadIdx.x, wave = tid >> 6;
-        const int64_t npairs = p.N >> 1;
-        const bool fast = p.x_aligned16 && p.small_n;
-        const int PAR = (int)(q_lo_of(p, 0) & 1);
+        // quad loads need dword alignment only (16-B loads at 8-B aligned sample offsets)
+        const bool fast = p.small_n && ((uintptr_t)p.x & 3) == 0;
+        const int kb = p.tap_scale_exp;
+        const int ld = lead(p);
         auto full = [&](int64_t t) {
-            const int64_t qb = q_lo_of(p, t) - PAR;
-            return fast && qb >= 0 && qb + 2 * NT * U <= p.N && (t + 1) * TS <= p.nout;
+            const int64_t q = q_lo_of(p, t);
+            return fast && q >= 0 && q + 4 * NQ <= p.N && t * TS >= ld && (t + 1) * TS - ld <= p.nout;
         };
-        Raw pre[U];
+        QT pre[U];
         // Base clamped into the chunk; issued when this workgroup has a next tile (a non-full
         // next tile is restaged). The epilogue's stores stay unconditional, so the next trip's
         // vmcnt waits remain counted.
         auto prefetch = [&](int64_t t) {
-            int64_t base = (q_lo_of(p, t) - PAR) >> 1;
-            base = base > npairs - NT * U ? npairs - NT * U : base;
-            const Raw* xb = reinterpret_cast<const Raw*>(p.x) + base;
+            int64_t base = q_lo_of(p, t);
+            base = base > p.N - 4 * NQ ? p.N - 4 * NQ : base;
 #pragma unroll
-            for (int u = 0; u < U; ++u) pre[u] = xb[tid + NT * u];
+            for (int u = 0; u < U; ++u) {
+                int e0 = 4 * (tid + NT * u);
+                if ((u + 1) * NT > NQ) e0 = e0 < 4 * (NQ - 1) ? e0 : 4 * (NQ - 1);   // spare lanes
+                pre[u] = Q::load(p.x, base + e0);
+            }
         };
         int64_t t = t0;
         while (t < t1) {
@@ -463,22 +607,20 @@ struct RxMfma {
                 prefetch(t);
                 for (; t < t1 && full(t); ++t) {
                     const int64_t n_lo = q_lo_of(p, t) + p.n_start;
-                    const uint32_t nb32 = (uint32_t)(p.c0 + (uint64_t)(n_lo - PAR));
-                    if (PAR) stage_fast<1>(p, lds, nb32, pre);   // uniform; no memory-counter ops inside
-                    else stage_fast<0>(p, lds, nb32, pre);
+                    const int ka = stage_fast(p, pl, red, (uint32_t)(p.c0 + (uint64_t)n_lo), pre, n_lo - p.n_start);
                     __syncthreads();
                     if (t + 1 < t1) prefetch(t + 1);       // next samples fly during the MFMAs
                     f32x4 dre, dim;
-                    fir(lds, bf, dre, dim);
-                    emit_full<EM>(p, t * TS + wave * 256, dre, dim);
+                    fir(pl, tbl, dre, dim);
+                    emit_full<EM>(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
                     __syncthreads();                       // LDS is restaged next trip
                 }
             } else {
-                stage_slow(p, lds, q_lo_of(p, t));
+                const int ka = stage_slow(p, pl, red, q_lo_of(p, t));
                 __syncthreads();
                 f32x4 dre, dim;
-                fir(lds, bf, dre, dim);
-                emit_edge(p, t * TS + wave * 256, dre, dim);
+                fir(pl, tbl, dre, dim);
+                emit_edge(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
                 __syncthreads();
                 ++t;
             }
@@ -487,25 +629,28 @@ struct RxMfma {
 };
 
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
-__global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const float* __restrict__ bfrag) {
+__global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
     using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
+    _Float16* pl = lds_h;                                   // 4 sample planes
+    _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
+    float* red = reinterpret_cast<float*>(tbl + K::NC * 2 * K::TB);
     if (blockIdx.x == 0) rx_state_update<InT>(p);
-    float* bf = reinterpret_cast<float*>(lds + K::LDS_SAMPLES);   // band table, read-only below
-    for (int j = threadIdx.x; j < K::TBL; j += K::NT) bf[j] = bfrag[j];
+    for (int j = threadIdx.x; j < K::NC * 2 * K::TB / 8; j += K::NT)
+        reinterpret_cast<h8*>(tbl)[j] = reinterpret_cast<const h8*>(tables)[j];
     __syncthreads();
-    const int64_t ntiles = (p.nout + K::TS - 1) / K::TS;
+    const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;
     const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
     if (t0 >= t1) return;
     // f32 input with the complex mix (the loopback chain): the epilogue is specialised on what
     // it stores, so the tile loop's store count is static. Other variants share the guarded one.
     if (std::is_same<InT, float>::value && MIX == MIX_COMPLEX) {
         const bool qam = p.slicer_kind == SLICER_QAM_AXIS && p.out_sym;
-        if (p.out_iq && qam) { K::template run<RXE_IQSYM>(p, lds, bf, t0, t1); return; }
-        if (p.out_iq && !p.out_sym) { K::template run<RXE_IQ>(p, lds, bf, t0, t1); return; }
-        if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, lds, bf, t0, t1); return; }
+        if (p.out_iq && qam) { K::template run<RXE_IQSYM>(p, pl, tbl, red, t0, t1); return; }
+        if (p.out_iq && !p.out_sym) { K::template run<RXE_IQ>(p, pl, tbl, red, t0, t1); return; }
+        if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, pl, tbl, red, t0, t1); return; }
     }
-    K::template run<RXE_GEN>(p, lds, bf, t0, t1);
+    K::template run<RXE_GEN>(p, pl, tbl, red, t0, t1);
 }
 
 // Any decimation: thread per kept instant, mixed samples staged in natural order.
@@ -572,43 +717,43 @@ static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s
 }
 
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
-static hipError_t rxm_go(const RxParams& p, const float* bfrag, hipStream_t s) {
-    using C = RxMfmaCfg<DEC>;
+static hipError_t rxm_go(const RxParams& p, const void* tables, hipStream_t s) {
     using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
-    const int64_t ntiles = (p.nout + C::TS - 1) / C::TS;
-    const size_t lds = (size_t)K::LDS_SAMPLES * sizeof(float2) + (size_t)K::TBL * sizeof(float);
+    const int64_t ntiles = (p.nout + (p.k_first & 15) + K::TS - 1) / K::TS;
+    const size_t lds = K::LDS_BYTES;
     const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT>);
-    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT>), dim3(persistent_grid(k, C::NT, lds, ntiles)),
-                       dim3(C::NT), lds, s, p, bfrag);
+    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
+                       dim3(K::NT), lds, s, p, static_cast<const _Float16*>(tables));
     return hipGetLastError();
 }
 
+// (decim, k-steps) variants: W = 32 * nks >= 15 * decim + ntaps.
+#define RXM_TABLE(X) X(2, 2) X(2, 3) X(2, 5) X(2, 8) X(4, 3) X(4, 4) X(4, 6) X(4, 8) X(8, 5) X(8, 6) X(8, 9) X(8, 20)
+
 template <typename InT, int MIX, typename OutT>
-static hipError_t rxm_sel(const RxParams& p, int decim, int nks, const float* bfrag, hipStream_t s) {
-#define RXM(D, N) if (decim == D && nks == N) return rxm_go<D, N, InT, MIX, OutT>(p, bfrag, s);
-    RXM(4, 24) RXM(4, 32) RXM(4, 48) RXM(2, 16) RXM(2, 24) RXM(2, 40) RXM(8, 40) RXM(8, 48) RXM(8, 64)
+static hipError_t rxm_sel(const RxParams& p, int decim, int nks, const void* tables, hipStream_t s) {
+#define RXM(D, N) if (decim == D && nks == N) return rxm_go<D, N, InT, MIX, OutT>(p, tables, s);
+    RXM_TABLE(RXM)
 #undef RXM
     return hipErrorInvalidValue;
 }
 
 int rx_mfma_ksteps(int decim, int L) {
-    const int need = (15 * decim + L + 3) / 4;
-    int cand[3] = {0, 0, 0};
-    if (decim == 4) { cand[0] = 24; cand[1] = 32; cand[2] = 48; }
-    else if (decim == 2) { cand[0] = 16; cand[1] = 24; cand[2] = 40; }
-    else if (decim == 8) { cand[0] = 40; cand[1] = 48; cand[2] = 64; }
-    for (int n : cand)
-        if (n >= need) return n;
-    return 0;
+    const int need = (15 * decim + L + 31) / 32;
+    int best = 0;
+#define RXK(D, N) if (decim == D && N >= need && (best == 0 || N < best)) best = N;
+    RXM_TABLE(RXK)
+#undef RXK
+    return best;
 }
 
-hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const float* bfrag, int in_dtype,
+hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const void* tables, int in_dtype,
                           int out_dtype, int mix, hipStream_t s) {
     auto go = [&](auto in_t, auto out_t) {
         using InT = decltype(in_t);
         using OutT = decltype(out_t);
-        return mix == MIX_REFERENCE_REAL ? rxm_sel<InT, MIX_REFERENCE_REAL, OutT>(p, decim, nks, bfrag, s)
-                                         : rxm_sel<InT, MIX_COMPLEX, OutT>(p, decim, nks, bfrag, s);
+        return mix == MIX_REFERENCE_REAL ? rxm_sel<InT, MIX_REFERENCE_REAL, OutT>(p, decim, nks, tables, s)
+                                         : rxm_sel<InT, MIX_COMPLEX, OutT>(p, decim, nks, tables, s);
     };
     if (in_dtype == 1) return out_dtype == 1 ? go(__half(), __half()) : go(__half(), float());
     return out_dtype == 1 ? go(float(), __half()) : go(float(), float());
