@@ -403,6 +403,8 @@ struct RxMfma {
     static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
     static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 16;
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
+    static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
+    static constexpr int SLOT_POS = 4 * NT + 8 * (4 * NT / RW);   // plane offset between slots
 
     // Rows hold 16 instants aligned to the absolute instant index (k % 16 == column), so an
     // instant's taps always fall at the same k positions of the 32-wide MFMA sums and the
@@ -413,14 +415,14 @@ struct RxMfma {
         return (p.k_first - lead(p) + t * TS) * DEC + p.D + 15 * DEC - W + 1 - p.n_start;
     }
 
-    // Scale, split and write samples e0..e0+3 (e0 % 4 == 0: one row, 8-B aligned).
-    __device__ static void put4(_Float16* pl, int e0, const float (&zr)[4], const float (&zi)[4], float sc) {
+    // Scale, split and write samples e0..e0+3 at plane offset o = rxh_pos(e0) (e0 % 4 == 0:
+    // one row, 8-B aligned).
+    __device__ static void put4o(_Float16* pl, int o, const float (&zr)[4], const float (&zi)[4], float sc) {
         h2 rh0, rl0, rh1, rl1, ih0, il0, ih1, il1;
         split2((cf2){zr[0], zr[1]} * sc, rh0, rl0);
         split2((cf2){zr[2], zr[3]} * sc, rh1, rl1);
         split2((cf2){zi[0], zi[1]} * sc, ih0, il0);
         split2((cf2){zi[2], zi[3]} * sc, ih1, il1);
-        const int o = rxh_pos(e0, RW);
         *reinterpret_cast<h4*>(pl + o) = (h4){rh0.x, rh0.y, rh1.x, rh1.y};
         *reinterpret_cast<h4*>(pl + PL + o) = (h4){rl0.x, rl0.y, rl1.x, rl1.y};
         *reinterpret_cast<h4*>(pl + 2 * PL + o) = (h4){ih0.x, ih0.y, ih1.x, ih1.y};
@@ -428,15 +430,17 @@ struct RxMfma {
     }
 
     // Steady state: the tile's samples lie inside the chunk, carrier index < 2^32. Staged
-    // at scale 1 (the tile max is tracked on the way); a tile whose max falls outside
-    // [2^-3, 2^15) is restaged scaled by stage_slow. Returns the tile's scale exponent ka.
+    // at scale 1 (the tile max is tracked on the way). Returns the tile's scale exponent: 0,
+    // or for a tile whose max falls outside [2^-3, 2^15) the exponent the general path
+    // (stage_slow) must restage it with.
     __device__ static int stage_fast(const RxParams& p, _Float16* pl, float* red, uint32_t nb32,
-                                     const QT (&pre)[U], int64_t q_lo) {
+                                     const QT (&pre)[U]) {
         const int tid = threadIdx.x;
         // carrier index of the lane's first sample; opaque, so that the per-sample offsets
         // stay immediates instead of 4*U hoisted loop-invariant VGPRs
         uint32_t lb = nb32 + 4u * (uint32_t)tid;
-        asm volatile("" : "+v"(lb));
+        int pos0 = rxh_pos(4 * tid, RW);                  // slot u writes at pos0 + u * SLOT_POS
+        asm volatile("" : "+v"(lb), "+v"(pos0));
         float mx = 0.f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -461,14 +465,10 @@ struct RxMfma {
                 if ((u + 1) * 4 * NT <= NS || e0 + j < NS)
                     mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(zr[j]), __builtin_fabsf(zi[j])));
             }
-            if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, e0, zr, zi, 1.0f);
+            if ((u + 1) * 4 * NT <= NS || e0 < NS) put4o(pl, pos0 + u * SLOT_POS, zr, zi, 1.0f);
         }
-        const int ka = tile_scale_exp(mx, red);
-        if (ka != 0) {                                      // rare: out-of-window magnitudes
-            __syncthreads();                                // `red` is reused
-            return stage_slow(p, pl, red, q_lo);
-        }
-        return 0;
+        // ka != 0 (rare: out-of-window magnitudes): the caller restages the tile scaled
+        return tile_scale_exp(mx, red);
     }
 
     // First / last tiles of a chunk, unaligned input, carrier index >= 2^32: per sample, two
@@ -490,7 +490,7 @@ struct RxMfma {
                                              : make_float2(0.f, 0.f);
                 zr[j] = z.x; zi[j] = z.y;
             }
-            put4(pl, e0, zr, zi, sc);
+            put4o(pl, rxh_pos(e0, RW), zr, zi, sc);
         }
         return ka;
     }
@@ -498,7 +498,7 @@ struct RxMfma {
     // One 16x16 tile per wave. Lane (i = lane & 15, g = lane >> 4) reads A row i, samples
     // 32s + 8g .. +7, and B[32s + 8g + j][c = i] = T[32s + 8g + j + (15 - c)*DEC].
     __device__ static void fir(const _Float16* pl, const _Float16* tbl, f32x4& dre, f32x4& dim) {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const int i = lane & 15, g = lane >> 4;
         const _Float16* arow = pl + (16 * wave + i) * RP + 8 * g;
         const int xb = 8 * g + (15 - i) * DEC;                  // B start for this lane's column
@@ -548,16 +548,20 @@ struct RxMfma {
         for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(dre[r]), "v"(dim[r]));
         return;
 #endif
+        // uniform base pointers + 32-bit lane offsets: saddr + voffset stores, no 64-bit
+        // per-lane address registers
+        OutT* qb = reinterpret_cast<OutT*>(p.out_iq) + 2 * ot;
+        uint8_t* sb = p.out_sym + ot;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            const uint32_t off = (uint32_t)(16 * (4 * (lane >> 4) + r) + (lane & 15));
             const float re = GAIN * __builtin_ldexpf(dre[r], -kab), im = GAIN * __builtin_ldexpf(dim[r], -kab);
             if (EM == RXE_GEN) {
                 rx_emit<OutT>(p, ot + off, re, im);
                 continue;
             }
-            if (EM & RXE_IQ) OutIO<OutT>::store_one(p.out_iq, ot + off, re, im);
-            if (EM & RXE_SYM) p.out_sym[ot + off] = rx_slice_qam(p, re, im);
+            if (EM & RXE_IQ) OutIO<OutT>::store_one(qb, off, re, im);
+            if (EM & RXE_SYM) sb[off] = rx_slice_qam(p, re, im);
         }
     }
 
@@ -578,7 +582,7 @@ struct RxMfma {
     template <int EM>
     __device__ static void run(const RxParams& p, _Float16* pl, const _Float16* tbl, float* red,
                                int64_t t0, int64_t t1) {
-        const int tid = threadIdx.x, wave = tid >> 6;
+        const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar
         // quad loads need dword alignment only (16-B loads at 8-B aligned sample offsets)
         const bool fast = p.small_n && ((uintptr_t)p.x & 3) == 0;
         const int kb = p.tap_scale_exp;
@@ -594,28 +598,41 @@ struct RxMfma {
         auto prefetch = [&](int64_t t) {
             int64_t base = q_lo_of(p, t);
             base = base > p.N - 4 * NQ ? p.N - 4 * NQ : base;
+            int l0 = 4 * tid;                               // opaque: no per-slot hoisted addresses
+            asm volatile("" : "+v"(l0));
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                int e0 = 4 * (tid + NT * u);
+                int e0 = l0 + 4 * NT * u;
                 if ((u + 1) * NT > NQ) e0 = e0 < 4 * (NQ - 1) ? e0 : 4 * (NQ - 1);   // spare lanes
+#ifdef MODEM_ABLATE_LOAD
+                float v = (float)(base + e0);
+                asm volatile("" : "+v"(v));
+                if constexpr (std::is_same<InT, float>::value) pre[u] = QT{make_float4(v, v, v, v), make_float4(v, v, v, v)};
+                else pre[u] = make_uint4(__float_as_uint(v), 0, 0, 0);
+#else
                 pre[u] = Q::load(p.x, base + e0);
+#endif
             }
         };
         int64_t t = t0;
+        bool restage = false;
         while (t < t1) {
-            if (full(t)) {
+            if (full(t) && !restage) {
                 prefetch(t);
                 for (; t < t1 && full(t); ++t) {
                     const int64_t n_lo = q_lo_of(p, t) + p.n_start;
-                    const int ka = stage_fast(p, pl, red, (uint32_t)(p.c0 + (uint64_t)n_lo), pre, n_lo - p.n_start);
+                    const int ka = stage_fast(p, pl, red, (uint32_t)(p.c0 + (uint64_t)n_lo), pre);
+                    if (ka != 0) { restage = true; break; }       // uniform; leaves the loop
                     __syncthreads();
                     if (t + 1 < t1) prefetch(t + 1);       // next samples fly during the MFMAs
                     f32x4 dre, dim;
                     fir(pl, tbl, dre, dim);
-                    emit_full<EM>(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
+                    emit_full<EM>(p, t * TS + wave * 256 - ld, dre, dim, kb);
                     __syncthreads();                       // LDS is restaged next trip
                 }
             } else {
+                __syncthreads();                           // `red` and the planes are reused
+                restage = false;
                 const int ka = stage_slow(p, pl, red, q_lo_of(p, t));
                 __syncthreads();
                 f32x4 dre, dim;

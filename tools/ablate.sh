@@ -1,13 +1,21 @@
 #!/bin/bash
 # Build ablation variants of the backend (profiling only) into rust-modem_amd/build/ablate/<v>/.
-# Each variant drops one stage of the kernels so its cost shows up as a time difference.
+# Each variant drops one stage of the kernels so its cost shows up as a time difference:
+# FIR (no matrix products), TRIG (no sin/cos), MIX (no carrier mix at all), STORE (no
+# output stores), LOAD (RX: no input loads). Usage: tools/ablate.sh [variants...]
 set -e
 cd "$(dirname "$0")/../rust-modem_amd"
-for v in base FIR TRIG MIX STORE; do
+vars=${@:-base FIR TRIG MIX STORE LOAD}
+for v in $vars; do
   d=build/ablate/$v; mkdir -p $d
   extra=""; [ "$v" != base ] && extra="-DMODEM_ABLATE_$v"
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 $extra -c csrc/modem_kernels.hip -o $d/k.o &
+  for f in tx rx misc; do
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 $extra -c csrc/modem_$f.hip -o $d/$f.o &
+  done
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -x hip -c csrc/modem_capi.cpp -o $d/c.o &
-  wait
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $d/k.o $d/c.o -o $d/libmodem_hip.so
+done
+wait
+for v in $vars; do
+  d=build/ablate/$v
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $d/tx.o $d/rx.o $d/misc.o $d/c.o -o $d/libmodem_hip.so
 done

@@ -2,7 +2,7 @@
 # Time every ablation variant (run on the GPU box): kernel-trace stats per variant.
 export TMPDIR=/tmp
 cfg=${1:-c3}
-for v in base FIR TRIG MIX STORE; do
+for v in ${VARIANTS:-base FIR TRIG MIX STORE LOAD}; do
   RUST_MODEM_AMD_LIB=$PWD/rust-modem_amd/build/ablate/$v/libmodem_hip.so timeout -k 10 200 \
     rocprofv3 --kernel-trace --stats -d gpurun_out/abl_$v -o run --output-format csv -- \
     python3 tools/prof_kernels.py --config $cfg --reps 20 > gpurun_out/abl_$v.log 2>&1
