@@ -341,7 +341,22 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 // hi = rn_f16(v), lo = rn_f16(v - hi) for two values (v - hi is exact in f32).
 __device__ __forceinline__ void split2(cf2 v, h2& hi, h2& lo) {
     hi = __builtin_convertvector(v, h2);
-    lo = __builtin_convertvector(v - __builtin_convertvector(hi, cf2), h2);
+    float l0, l1;                                   // v - hi, exact: one v_fma_mix_f32 each
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l0) : "v"(hi), "v"(v.x));
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(l1) : "v"(hi), "v"(v.y));
+    lo = __builtin_convertvector((cf2){l0, l1}, h2);
+}
+
+// Conjugate mix of one sample, packed: (re, im) = (x*cs + y*sn, y*cs - x*sn) with the same
+// roundings as fma(y, sn, x*cs) / fma(-x, sn, y*cs). cssn = (cs, sn), typically straight from
+// v_sin/v_cos: gfx950 needs one wait state before a VALU reads a transcendental's result, and
+// the compiler's hazard recognizer does not look inside inline asm, hence the s_nop.
+__device__ __forceinline__ cf2 cmix(cf2 x, cf2 cssn) {
+    cf2 t, z;
+    asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(x), "v"(cssn));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
+        : "=v"(z) : "v"(x), "v"(cssn), "v"(t));
+    return z;
 }
 
 // Four consecutive input samples (one lane's staging quad).
@@ -458,14 +473,15 @@ struct RxMfma {
 #endif
                 if (MIX == MIX_REFERENCE_REAL) { zr[j] = x[j].x * cs; zi[j] = x[j].x * -sn; }
                 else {
-                    zr[j] = __builtin_fmaf(x[j].y, sn, x[j].x * cs);
-                    zi[j] = __builtin_fmaf(-x[j].x, sn, x[j].y * cs);
+                    const cf2 z = cmix((cf2){x[j].x, x[j].y}, (cf2){cs, sn});
+                    zr[j] = z.x; zi[j] = z.y;
                 }
                 // only the last slot can reach past the tile: its extra samples are not counted
-                if ((u + 1) * 4 * NT <= NS || e0 + j < NS)
-                    mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(zr[j]), __builtin_fabsf(zi[j])));
+                if ((u + 1) * 4 * NT <= NS || e0 + j < NS)      // one v_max3 per sample
+                    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j]), "v"(zi[j]));
             }
             if ((u + 1) * 4 * NT <= NS || e0 < NS) put4o(pl, pos0 + u * SLOT_POS, zr, zi, 1.0f);
+            __builtin_amdgcn_sched_barrier(0);              // one quad's temporaries at a time
         }
         // ka != 0 (rare: out-of-window magnitudes): the caller restages the tile scaled
         return tile_scale_exp(mx, red);
