@@ -293,13 +293,16 @@ struct modem_tx {
     float2* d_hist[2] = {nullptr, nullptr};
     uint8_t* d_carry[2] = {nullptr, nullptr};
     int hcur = 0, ccur = 0, ncarry = 0;
-    int mfma_ksteps = 0;            // > 0: FIR on the matrix pipe (tx_mfma)
-    float* d_bfrag = nullptr;       // its per-lane B fragments [ksteps][64]
+    int mfma_ksteps = 0;            // > 0: FIR on the matrix cores (tx_mfma)
+    float* d_bfrag = nullptr;       // its split-f16 per-lane B fragments (modem_internal.h)
+    float* d_luth = nullptr;        // its split-f16 LUT (re_hi, re_lo, im_hi, im_lo per entry)
+    int lut_scale_exp = 0, tap_scale_exp = 0;
+    uint64_t symbols = 0;           // symbols emitted so far (row-block alignment)
     Stage bits_stage, out_stage;
     ~modem_tx() {
         DeviceGuard g(device);
         for (void* p : {(void*)d_lut, (void*)d_taps, (void*)d_hist[0], (void*)d_hist[1],
-                        (void*)d_carry[0], (void*)d_carry[1], (void*)d_bfrag})
+                        (void*)d_carry[0], (void*)d_carry[1], (void*)d_bfrag, (void*)d_luth})
             if (p) (void)hipFree(p);
     }
 };
@@ -355,20 +358,45 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     // MODEM_HIP_FIR=valu forces the packed-VALU kernel (both are parity-tested).
     const char* env = std::getenv("MODEM_HIP_FIR");
     const bool force_valu = env && std::strcmp(env, "valu") == 0;
-    h->mfma_ksteps = force_valu ? 0 : mk::tx_mfma_ksteps((int)h->sps, (int)h->K);
+    // Sample-and-hold (no taps) stays on the VALU kernels, which reproduce it bit for bit.
+    h->mfma_ksteps = (force_valu || d->ntaps == 0) ? 0 : mk::tx_mfma_ksteps((int)h->sps, (int)h->K);
     if (h->mfma_ksteps > 0) {
-        // B[o][j] = h[p + sps*(c + PRE - o)], j = sps*c + p, for lane l / k-step s:
-        // o = 4s + (l >> 4), j = l & 15 (tx_mfma in modem_kernels.hip).
-        const int nks = h->mfma_ksteps, sps = (int)h->sps, SB = 16 / sps, PRE = 4 * nks - SB;
-        std::vector<float> bf((size_t)nks * 64, 0.0f);
-        for (int st = 0; st < nks; ++st)
-            for (int l = 0; l < 64; ++l) {
-                const int o = 4 * st + (l >> 4), j = l & 15, c = j / sps, ph = j % sps;
-                const int t = c + PRE - o;
-                if (t >= 0 && t < (int)h->K) bf[(size_t)st * 64 + l] = pp[(size_t)t * sps + ph];
-            }
-        if ((st = dalloc(&h->d_bfrag, bf.size()))) { delete h; return st; }
-        if (hipMemcpy(h->d_bfrag, bf.data(), bf.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        // Split-f16 operands of tx_mfma (modem_tx.hip). Exact power-of-two scales put the
+        // maxima of the LUT and of the taps in [2^14, 2^15); both are split hi + lo =
+        // rn_f16(v) + rn_f16(v - hi).
+        auto scale_exp = [](float mx) {
+            int e = 0;
+            if (mx > 0.0f && std::isfinite(mx)) { std::frexp(mx, &e); return 15 - e; }
+            return 0;
+        };
+        auto split = [](float v, _Float16& hi, _Float16& lo) { hi = (_Float16)v; lo = (_Float16)(v - (float)hi); };
+        float lmax = 0.0f, tmax = 0.0f;
+        for (size_t k = 0; k < 2 * nl; ++k) lmax = std::max(lmax, std::fabs(d->lut[k]));
+        for (uint32_t k = 0; k < d->ntaps; ++k) tmax = std::max(tmax, std::fabs(d->taps[k]));
+        h->lut_scale_exp = scale_exp(lmax);
+        h->tap_scale_exp = scale_exp(tmax);
+        std::vector<_Float16> lh(4 * nl);
+        for (size_t k = 0; k < nl; ++k) {
+            split(std::ldexp(d->lut[2 * k], h->lut_scale_exp), lh[4 * k], lh[4 * k + 1]);
+            split(std::ldexp(d->lut[2 * k + 1], h->lut_scale_exp), lh[4 * k + 2], lh[4 * k + 3]);
+        }
+        // B[o][j] = h[p + sps*(c + PRE - o)], j = sps*c + p: lane l holds, for k-step s, the 8
+        // window offsets o = 32s + 8(l >> 4) + jj of column j = l & 15, hi then lo.
+        const int nks = h->mfma_ksteps, sps = (int)h->sps, SB = 16 / sps, PRE = 32 * nks - SB;
+        std::vector<_Float16> bf((size_t)nks * 2 * 64 * 8, (_Float16)0.0f);
+        for (int s2 = 0; s2 < nks; ++s2)
+            for (int l = 0; l < 64; ++l)
+                for (int jj = 0; jj < 8; ++jj) {
+                    const int o = 32 * s2 + 8 * (l >> 4) + jj, j = l & 15, c = j / sps, ph = j % sps;
+                    const int t = c + PRE - o;
+                    const float v = (t >= 0 && t < (int)h->K) ? std::ldexp(pp[(size_t)t * sps + ph], h->tap_scale_exp) : 0.0f;
+                    split(v, bf[(((size_t)s2 * 2) * 64 + l) * 8 + jj], bf[(((size_t)s2 * 2 + 1) * 64 + l) * 8 + jj]);
+                }
+        const size_t nb = (bf.size() * sizeof(_Float16) + sizeof(float) - 1) / sizeof(float);
+        const size_t nlh = (lh.size() * sizeof(_Float16) + sizeof(float) - 1) / sizeof(float);
+        if ((st = dalloc(&h->d_bfrag, nb)) || (st = dalloc(&h->d_luth, nlh))) { delete h; return st; }
+        if (hipMemcpy(h->d_bfrag, bf.data(), bf.size() * sizeof(_Float16), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(h->d_luth, lh.data(), lh.size() * sizeof(_Float16), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipGetLastError();
             delete h;
             return MODEM_ERR_HIP;
@@ -427,6 +455,11 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
                    ((uintptr_t)dbits % h->bps) == 0) ? 1 : 0;
     p.small_n = (h->sample + nsamp) <= (1ull << 32) ? 1 : 0;
     p.w = h->w;
+    p.lut_h = h->d_luth;
+    p.lut_scale_exp = h->lut_scale_exp;
+    p.tap_scale_exp = h->tap_scale_exp;
+    const uint32_t sb = (h->sps <= 16 && 16 % h->sps == 0) ? 16 / h->sps : 1;   // symbols per row-block
+    p.lead = (int)(h->symbols % sb);
     if (h->mfma_ksteps > 0)
         HIP_TRY(mk::launch_tx_mfma(p, (int)h->sps, h->mfma_ksteps, h->d_bfrag, h->dtype, h->out_mode, s));
     else
@@ -434,6 +467,7 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     h->hcur ^= 1;
     if (!flush) { h->ccur ^= 1; h->ncarry = ncarry_new; }
     h->sample += nsamp;
+    h->symbols += (uint64_t)nsym;
     if (host_out) {
         HIP_TRY(hipMemcpyAsync(out, dout, nsamp * tx_sample_bytes(h), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));

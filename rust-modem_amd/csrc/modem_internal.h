@@ -30,6 +30,12 @@ struct TxParams {
     int32_t fast_bits;       // ncarry == 0, bps in {1,2,4,8}, bits aligned to bps bytes
     int32_t small_n;         // every carrier index of this call is < 2^32
     float w;                 // Freq::sample_freq()
+    // tx_mfma (split-f16 FIR): LUT as (re_hi, re_lo, im_hi, im_lo) halves of lut * 2^lut_scale_exp,
+    // B fragments hold taps * 2^tap_scale_exp; lead = symbols before this call, mod 16/sps.
+    const void* lut_h;
+    int32_t lut_scale_exp;
+    int32_t tap_scale_exp;
+    int32_t lead;
 };
 
 // One RX launch: input samples [0, N) (stream indices n_start ..), outputs k_first ..
@@ -75,10 +81,10 @@ struct FirParams {
 // Launchers return hipSuccess or the launch error. They pick a specialised kernel for the
 // common samples-per-symbol values and a generic one otherwise.
 hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s);
-// TX FIR on the matrix pipe: ksteps = window k-steps for (sps, K) or 0 when unsupported;
-// bfrag = per-lane B fragments [ksteps][64] (see tx_mfma in modem_kernels.hip).
+// TX FIR on the matrix cores (tx_mfma, split-f16 MFMA): 32-symbol k-steps for (sps, K), or 0
+// when no variant fits; bfrag = per-lane B fragments [ksteps][hi, lo][64 lanes][8 halves].
 int tx_mfma_ksteps(int sps, int K);
-hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const float* bfrag, int dtype,
+hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const void* bfrag, int dtype,
                           int out_mode, hipStream_t s);
 // RX matched filter on the matrix cores (rx_mfma, split-f16 MFMA): 32-sample k-steps for
 // (decim, ntaps), or 0 when no variant fits.

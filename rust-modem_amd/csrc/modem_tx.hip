@@ -263,30 +263,42 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
 }
 
 // ----------------------------------------------------------------------- TX on MFMA ----
-// The zero-stuffed polyphase FIR as f32 matrix products (v_mfma_f32_16x16x4_f32 is an exact
-// k-ordered fmaf chain, the same arithmetic as the VALU path, on the matrix pipe, leaving the
-// VALU to the bit-exact carrier phase, sin/cos and mix):
+// The zero-stuffed polyphase FIR on the matrix cores (v_mfma_f32_16x16x32_f16):
 //   rows i  = 16 row-blocks of SB = 16/SPS consecutive symbols,
 //   cols j  = (symbol c in the block, phase p) -> sample SPS*c + p of the block (16 samples),
-//   k  = o  = offset in a W = 4*NKS symbol window ending at the block's last symbol,
-//   A[i][o] = a[block_i - PRE + o]  (complex: one chain for re, one for im; from LDS),
-//   B[o][j] = h[p + SPS*(c + PRE - o)]  (banded tap matrix, constant: NKS VGPRs per lane).
-// MAC efficiency = (SB + K - 1) / W (0.92 for 129 taps at sps 4). One wave computes one
-// 16x16 output tile (256 samples) per 2*NKS MFMAs.
+//   k  = o  = offset in a W = 32*NKS symbol window ending at the block's last symbol,
+//   A[i][o] = a[block_i - PRE + o] (symbol values, from LDS), B[o][j] = h[p + SPS*(c + PRE - o)].
+// As on the RX, every operand is split in two f16 halves (a = a_hi + a_lo, round to nearest)
+// and A*B ~= A_hi*B_hi + A_hi*B_lo + A_lo*B_hi accumulates in f32 (6 MFMAs per k-step for the
+// re and im rails). The LUT and the taps are scaled by exact powers of two on the host
+// (2^lut_scale_exp, 2^tap_scale_exp: maxima in [2^14, 2^15)), split there, and the outputs
+// are scaled back with ldexp. Row-blocks are aligned to the absolute symbol index
+// (lead = symbols before this call, mod SB), so a symbol always meets the same taps at the
+// same k positions and a stream cut into calls gives the same samples as one call.
+// Sample-and-hold (no taps) stays on the exact VALU kernels.
 template <int SPS> struct TxMfmaCfg {
     static constexpr int SB = 16 / SPS;          // symbols per row-block
     static constexpr int NT = 256;               // 4 waves
     static constexpr int SUB = 4;                // 16x16 tiles per wave per tile
     static constexpr int TS = 4 * SUB * 16 * SB; // symbols per workgroup tile
+    static constexpr int NCOP = SB % 4 == 0 ? 1 : 4 / SB;   // plane copies (8-B aligned A reads)
 };
+
+typedef _Float16 th8 __attribute__((ext_vector_type(8)));
+typedef _Float16 th4 __attribute__((ext_vector_type(4)));
 
 template <int SPS, int NKS, int OUT_MODE, typename OutT>
 struct TxMfma {
     using C = TxMfmaCfg<SPS>;
-    static constexpr int SB = C::SB, NT = C::NT, SUB = C::SUB, TS = C::TS;
-    static constexpr int PRE = 4 * NKS - SB;       // window symbols before a row-block
+    static constexpr int SB = C::SB, NT = C::NT, SUB = C::SUB, TS = C::TS, NCOP = C::NCOP;
+    static constexpr int W = 32 * NKS;             // window symbols per row-block
+    static constexpr int PRE = W - SB;             // window symbols before a row-block
     static constexpr int NE = TS + PRE;            // symbols staged per tile
-    static constexpr int U = (NE + NT - 1) / NT;   // prefetched staging slots per lane
+    static constexpr int U = (NE + NT - 1) / NT;   // staging slots per lane
+    static constexpr int PLN = (NE + 3 * 4 + 7) & ~7;   // halves per plane copy
+    // LDS: NCOP copies x 4 planes (re_hi, re_lo, im_hi, im_lo) of PLN halves, then the split
+    // LUT (4 halves per entry)
+    static constexpr int PLANES = NCOP * 4 * PLN;
 
     // Raw bits word of symbol m, BPS bytes (fast path: aligned, no leftover bits).
     template <int BPS>
@@ -298,35 +310,92 @@ struct TxMfma {
         return *reinterpret_cast<const uint64_t*>(b);
     }
 
-    // Slow staging: first tile (filter history), leftover bits, flush, any bps.
-    __device__ static void stage_slow(const TxParams& p, float2* lds, const float2* lut_s, int64_t m0) {
-        for (int e = threadIdx.x; e < NE; e += NT) {
-            const int64_t m = m0 - PRE + e;
-            lds[e] = m < 0 ? (m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f))
-                           : (m >= p.nsym_valid ? make_float2(0.f, 0.f) : lut_s[tx_symbol_index(p, m)]);
+    // Symbol e of the tile (window coordinates) into every plane copy: copy c holds symbol e
+    // at half index e + c*SB, so a row-block starting at blk*SB reads copy ((-blk*SB) mod 4)/SB
+    // 8-B aligned.
+    __device__ static void put(_Float16* pl, int e, th4 v) {
+#pragma unroll
+        for (int c = 0; c < NCOP; ++c) {
+            _Float16* q = pl + c * 4 * PLN + e + c * SB;
+            q[0] = v[0]; q[PLN] = v[1]; q[2 * PLN] = v[2]; q[3 * PLN] = v[3];
         }
     }
 
-    // FIR of this wave's sub-tile q: D = sum_s A_s B_s (see the comment above TxMfmaCfg).
-    __device__ static void fir(const float2* lds, int q, const float (&bf)[NKS], f32x4& dre, f32x4& dim) {
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        const int sb0 = (wave * SUB + q) * 16 * SB;
-        const float2* arow = lds + sb0 + SB * (lane & 15) + (lane >> 4);
-        dre = (f32x4){0.f, 0.f, 0.f, 0.f};
-        dim = dre;
-        mfma_chain<NKS, 4>(arow, [](int s) { return 4 * s; }, bf, dre, dim);
+    // f32 symbol value -> scaled (2^ka) split halves (re_hi, re_lo, im_hi, im_lo), as the host
+    // splits the LUT (round to nearest both times).
+    __device__ static th4 split_value(float2 v, int ka) {
+        const float r = __builtin_ldexpf(v.x, ka), i = __builtin_ldexpf(v.y, ka);
+        const _Float16 rh = (_Float16)r, ih = (_Float16)i;
+        return (th4){rh, (_Float16)(r - (float)rh), ih, (_Float16)(i - (float)ih)};
     }
 
-    // Full 16x16 tile, carrier index < 2^32: four independent chains, unconditional stores.
-    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim) {
+    // General staging: first tile (history), leftover bits, flush, any bps.
+    __device__ static void stage_slow(const TxParams& p, _Float16* pl, int64_t ms) {
+        for (int e = threadIdx.x; e < NE; e += NT) {
+            const int64_t m = ms + e;
+            float2 v;
+            if (m < 0) v = m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f);
+            else v = m >= p.nsym_valid ? make_float2(0.f, 0.f) : p.lut[tx_symbol_index(p, m)];
+            put(pl, e, split_value(v, p.lut_scale_exp));
+        }
+    }
+
+    // 16x16 sub-tile q of this wave: D = sum over the window of A*B (split products).
+    __device__ static void fir(const _Float16* pl, int q, const th8 (&bh)[NKS], const th8 (&bl)[NKS],
+                               f32x4& dre, f32x4& dim) {
+        const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int i = lane & 15, g = lane >> 4;
+        const int blk = (wave * SUB + q) * 16 + i;                  // row-block in the tile
+        const int cp = ((4 - ((blk * SB) & 3)) & 3) / (SB < 4 ? SB : 4);   // copy shifting the row to 8 B
+        const _Float16* ar = pl + (NCOP > 1 ? cp : 0) * 4 * PLN + blk * SB + (NCOP > 1 ? cp * SB : 0) + 8 * g;
+        typedef _Float16 tq4 __attribute__((ext_vector_type(4), aligned(8)));
+        auto ld8 = [](const _Float16* a) {                          // 8-B aligned 16-B read
+            const tq4 x = *reinterpret_cast<const tq4*>(a), y = *reinterpret_cast<const tq4*>(a + 4);
+            return (th8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+        };
+#ifdef MODEM_ABLATE_FIR
+        const th8 a0 = ld8(ar);
+        dre = (f32x4){(float)a0[0], 0.f, 0.f, 0.f};
+        dim = (f32x4){(float)bh[0][0], 0.f, 0.f, 0.f};
+        return;
+#endif
+        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0, m0 = r0, m1 = r0;
+        th8 a[2][4];
+        auto load = [&](int s, int slot) {
+            a[slot][0] = ld8(ar + 32 * s);
+            a[slot][1] = ld8(ar + PLN + 32 * s);
+            a[slot][2] = ld8(ar + 2 * PLN + 32 * s);
+            a[slot][3] = ld8(ar + 3 * PLN + 32 * s);
+        };
+        load(0, 0);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const int c = s & 1;
+            if (s + 1 < NKS) load(s + 1, c ^ 1);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bh[s], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bh[s], m0, 0, 0, 0);
+            r1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bl[s], r1, 0, 0, 0);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bl[s], m1, 0, 0, 0);
+            r1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], bh[s], r1, 0, 0, 0);
+            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], bh[s], m1, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        dre = r0 + r1;
+        dim = m0 + m1;
+    }
+
+    // Full 16x16 tile, carrier index < 2^32: unconditional stores. jt = call sample index of
+    // the sub-tile's first sample.
+    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, int kab) {
         const int lane = threadIdx.x & 63;
         const uint32_t nb = (uint32_t)(p.s0 + (uint64_t)jt);
         float zr[4], zi[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
-            zr[r] = dre[r];
-            zi[r] = dim[r];
+            const float yr = __builtin_ldexpf(dre[r], -kab), yi = __builtin_ldexpf(dim[r], -kab);
+            zr[r] = yr;
+            zi[r] = yi;
 #ifdef MODEM_ABLATE_MIX
             if (false) {
 #else
@@ -334,121 +403,128 @@ struct TxMfma {
 #endif
                 float sn, cs;
                 sincos_phase(phase_from_f(p.w, (float)(nb + (uint32_t)off)), sn, cs);
-                zr[r] = __builtin_fmaf(dre[r], cs, -(dim[r] * sn));
-                zi[r] = __builtin_fmaf(dre[r], sn, dim[r] * cs);
+                zr[r] = __builtin_fmaf(yr, cs, -(yi * sn));
+                zi[r] = __builtin_fmaf(yr, sn, yi * cs);
             }
         }
 #ifdef MODEM_ABLATE_STORE
 #pragma unroll
         for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(zr[r]), "v"(zi[r]));
 #else
+        OutT* ob = reinterpret_cast<OutT*>(p.out) + (OUT_MODE == OUT_REAL ? 1 : 2) * jt;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int64_t j = jt + 16 * (4 * (lane >> 4) + r) + (lane & 15);
-            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, j, zr[r]);
-            else OutIO<OutT>::store_one(p.out, j, zr[r], zi[r]);
+            const uint32_t off = (uint32_t)(16 * (4 * (lane >> 4) + r) + (lane & 15));
+            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(ob, off, zr[r]);
+            else OutIO<OutT>::store_one(ob, off, zr[r], zi[r]);
         }
 #endif
     }
 
-    // Partial tile or carrier index >= 2^32: guarded, 64-bit indices.
-    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim) {
+    // Partial tile, samples before the call, or carrier index >= 2^32: guarded.
+    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, int kab) {
         const int lane = threadIdx.x & 63;
         const int64_t jend = p.nsym * SPS;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
-            if (jt + off < jend)
-                tx_emit_off<OUT_MODE, OutT>(p, jt, off, make_float2(dre[r], dim[r]), make_float2(0.f, 0.f), false);
+            if (jt + off >= 0 && jt + off < jend)
+                tx_emit_off<OUT_MODE, OutT>(p, jt, off, make_float2(__builtin_ldexpf(dre[r], -kab),
+                                            __builtin_ldexpf(dim[r], -kab)), make_float2(0.f, 0.f), false);
         }
     }
 
-    // BPS > 0: bits aligned, no leftover bits, carrier index < 2^32 (the steady state).
-    // BPS == 0: the general path (slow staging, guarded epilogue).
+    // Tile t holds symbols [t*TS - lead, (t+1)*TS - lead) of the call. BPS > 0: bits aligned,
+    // no leftover bits, carrier index < 2^32 (the steady state); BPS == 0: general path only.
     template <int BPS>
-    __device__ static void run(const TxParams& p, float2* lds, const float2* lut_s, const float (&bf)[NKS],
-                               int64_t t0, int64_t t1) {
-        const int tid = threadIdx.x;
-        const int64_t nfull = p.nsym / TS;          // tiles with every sample inside the call
-        const int64_t tf = BPS > 0 ? (t1 < nfull ? t1 : nfull) : t0;
+    __device__ static void run(const TxParams& p, _Float16* pl, const th4* lut_s, const th8 (&bh)[NKS],
+                               const th8 (&bl)[NKS], int64_t t0, int64_t t1) {
+        const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int lead = p.lead;
+        const int kab = p.lut_scale_exp + p.tap_scale_exp;
         const int64_t mlast = p.nsym_valid - 1;
-        auto inside = [&](int64_t m0) { return m0 - PRE >= 0 && m0 + TS <= p.nsym_valid; };
+        // full tile: every staged symbol is data of this call, every sample is emitted
+        auto full = [&](int64_t t) {
+            const int64_t ms = t * TS - lead - PRE;
+            return BPS > 0 && ms >= 0 && ms + NE <= p.nsym_valid && t * TS - lead + TS <= p.nsym;
+        };
         uint64_t pre[U];
-        // Address clamped into the call's bits. Issued only when this workgroup has a next tile
-        // (a wasted tile per persistent workgroup is +25 % traffic); the stores after it stay
-        // unconditional, so the next trip's vmcnt waits remain counted.
-        auto prefetch = [&](int64_t m0) {
+        auto prefetch = [&](int64_t t) {
+            const int64_t ms = t * TS - lead - PRE;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                int64_t m = m0 - PRE + tid + NT * u;
+                int64_t m = ms + tid + NT * u;
                 m = m < 0 ? 0 : (m > mlast ? mlast : m);
                 pre[u] = load_word<BPS>(p.bits, m);
             }
         };
-        if (BPS > 0 && t0 < tf && mlast >= 0) prefetch(t0 * TS);
-        for (int64_t t = t0; t < tf; ++t) {
-            const int64_t m0 = t * TS;
-            if (inside(m0)) {
+        int64_t t = t0;
+        while (t < t1) {
+            if (full(t)) {
+                prefetch(t);
+                for (; t < t1 && full(t); ++t) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int e = tid + NT * u;
-                    if (e < NE) lds[e] = lut_s[word_index(pre[u], BPS)];
+                    for (int u = 0; u < U; ++u) {
+                        const int e = tid + NT * u;
+                        if (e < NE) put(pl, e, lut_s[word_index(pre[u], BPS)]);
+                    }
+                    __syncthreads();
+                    if (t + 1 < t1) prefetch(t + 1);     // next bits fly during the MFMAs
+                    const int64_t j0 = (t * TS - lead) * SPS;
+#pragma unroll
+                    for (int q = 0; q < SUB; ++q) {
+                        f32x4 dre, dim;
+                        fir(pl, q, bh, bl, dre, dim);
+                        emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, kab);
+                    }
+                    __syncthreads();                     // the window is restaged next trip
                 }
             } else {
-                stage_slow(p, lds, lut_s, m0);
-            }
-            __syncthreads();
-            if (t + 1 < tf) prefetch(m0 + TS);       // next bits fly during the MFMAs
-            // fully unrolled: a static store count lets the next trip wait vmcnt(#stores)
-            // for its prefetched bits instead of draining this tile's stores
-#pragma unroll
-            for (int q = 0; q < SUB; ++q) {
-                f32x4 dre, dim;
-                fir(lds, q, bf, dre, dim);
-                emit_full(p, (m0 + ((threadIdx.x >> 6) * SUB + q) * 16 * SB) * SPS, dre, dim);
-            }
-            __syncthreads();                         // the window is restaged next trip
-        }
-        for (int64_t t = tf > t0 ? tf : t0; t < t1; ++t) {   // partial / general tiles
-            const int64_t m0 = t * TS;
-            stage_slow(p, lds, lut_s, m0);
-            __syncthreads();
+                stage_slow(p, pl, t * TS - lead - PRE);
+                __syncthreads();
+                const int64_t j0 = (t * TS - lead) * SPS;
 #pragma unroll 1
-            for (int q = 0; q < SUB; ++q) {
-                f32x4 dre, dim;
-                fir(lds, q, bf, dre, dim);
-                emit_edge(p, (m0 + ((threadIdx.x >> 6) * SUB + q) * 16 * SB) * SPS, dre, dim);
+                for (int q = 0; q < SUB; ++q) {
+                    f32x4 dre, dim;
+                    fir(pl, q, bh, bl, dre, dim);
+                    emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, kab);
+                }
+                __syncthreads();
+                ++t;
             }
-            __syncthreads();
         }
     }
 };
 
 template <int SPS, int NKS, int OUT_MODE, typename OutT>
-__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const float* __restrict__ bfrag) {
+__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
     using K = TxMfma<SPS, NKS, OUT_MODE, OutT>;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2* lut_s = lds + ((K::NE + 1) & ~1);
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds_t[];
+    _Float16* pl = lds_t;
+    th4* lut_s = reinterpret_cast<th4*>(lds_t + K::PLANES);
     const int tid = threadIdx.x, lane = tid & 63;
     if (blockIdx.x == 0) tx_state_update(p);
-    for (int i = tid; i < (1 << p.bps); i += K::NT) lut_s[i] = p.lut[i];
-    float bf[NKS];                               // this lane's B fragments, one per k-step
+    const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
+    for (int i = tid; i < (1 << p.bps); i += K::NT) lut_s[i] = lut_h[i];
+    th8 bh[NKS], bl[NKS];                        // this lane's B fragments (hi, lo) per k-step
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) bf[s] = bfrag[s * 64 + lane];
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) pin(bf[s]);
+    for (int s = 0; s < NKS; ++s) {
+        bh[s] = bfrag[(2 * s) * 64 + lane];
+        bl[s] = bfrag[(2 * s + 1) * 64 + lane];
+    }
     __syncthreads();   // LUT visible
-    const int64_t ntiles = (p.nsym + K::TS - 1) / K::TS;
+    const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
     const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    if (t0 >= t1) return;
     if (p.fast_bits && p.small_n) {              // one uniform switch: the tile loop is specialised
         switch (p.bps) {
-        case 1: K::template run<1>(p, lds, lut_s, bf, t0, t1); return;
-        case 2: K::template run<2>(p, lds, lut_s, bf, t0, t1); return;
-        case 4: K::template run<4>(p, lds, lut_s, bf, t0, t1); return;
-        case 8: K::template run<8>(p, lds, lut_s, bf, t0, t1); return;
+        case 1: K::template run<1>(p, pl, lut_s, bh, bl, t0, t1); return;
+        case 2: K::template run<2>(p, pl, lut_s, bh, bl, t0, t1); return;
+        case 4: K::template run<4>(p, pl, lut_s, bh, bl, t0, t1); return;
+        case 8: K::template run<8>(p, pl, lut_s, bh, bl, t0, t1); return;
         }
     }
-    K::template run<0>(p, lds, lut_s, bf, t0, t1);
+    K::template run<0>(p, pl, lut_s, bh, bl, t0, t1);
 }
 
 // Any samples-per-symbol: thread per output sample, symbols staged in LDS.
@@ -517,41 +593,39 @@ static hipError_t tx_mode(const TxParams& p, int sps, int out_mode, hipStream_t 
 }
 
 template <int SPS, int NKS, int OM, typename OutT>
-static hipError_t txm_go(const TxParams& p, const float* bfrag, hipStream_t s) {
-    using C = TxMfmaCfg<SPS>;
-    constexpr int NE = TxMfma<SPS, NKS, OM, OutT>::NE;
-    const int64_t ntiles = (p.nsym + C::TS - 1) / C::TS;
-    const size_t lds = ((size_t)((NE + 1) & ~1) + ((size_t)1 << p.bps)) * sizeof(float2);
+static hipError_t txm_go(const TxParams& p, const void* bfrag, hipStream_t s) {
+    using K = TxMfma<SPS, NKS, OM, OutT>;
+    const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
+    const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << p.bps) * 8;
     const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT>);
-    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT>), dim3(persistent_grid(k, C::NT, lds, ntiles)),
-                       dim3(C::NT), lds, s, p, bfrag);
+    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
+                       dim3(K::NT), lds, s, p, static_cast<const th8*>(bfrag));
     return hipGetLastError();
 }
 
+// (sps, k-steps) variants: W = 32 * nks >= 16/sps + K - 1 symbols (K = taps per phase).
+#define TXM_TABLE(X) X(2, 1) X(2, 2) X(2, 3) X(2, 5) X(4, 1) X(4, 2) X(4, 3) X(4, 5) X(4, 9) \
+                     X(8, 1) X(8, 2) X(8, 3) X(8, 5) X(8, 9) X(16, 1) X(16, 2) X(16, 3) X(16, 5)
+
 template <int OM, typename OutT>
-static hipError_t txm_sel(const TxParams& p, int sps, int nks, const float* bfrag, hipStream_t s) {
+static hipError_t txm_sel(const TxParams& p, int sps, int nks, const void* bfrag, hipStream_t s) {
 #define TXM(S, N) if (sps == S && nks == N) return txm_go<S, N, OM, OutT>(p, bfrag, s);
-    TXM(4, 3) TXM(4, 5) TXM(4, 9) TXM(4, 17) TXM(4, 33)
-    TXM(8, 5) TXM(8, 9) TXM(8, 17) TXM(8, 33)
-    TXM(2, 5) TXM(2, 9) TXM(2, 17)
-    TXM(16, 3) TXM(16, 5) TXM(16, 9) TXM(16, 17)
+    TXM_TABLE(TXM)
 #undef TXM
     return hipErrorInvalidValue;
 }
 
 int tx_mfma_ksteps(int sps, int K) {
     if (sps != 2 && sps != 4 && sps != 8 && sps != 16) return 0;
-    const int need = (16 / sps + K - 1 + 3) / 4;
-    static const int steps[] = {3, 5, 9, 17, 33};
-    for (int n : steps) {
-        if (n < need) continue;
-        if ((sps == 8 && n == 3) || (sps == 2 && n == 3) || (sps == 2 && n == 33) || (sps == 16 && n == 33)) continue;
-        return n;
-    }
-    return 0;
+    const int need = (16 / sps + K - 1 + 31) / 32;
+    int best = 0;
+#define TXK(S, N) if (sps == S && N >= need && (best == 0 || N < best)) best = N;
+    TXM_TABLE(TXK)
+#undef TXK
+    return best;
 }
 
-hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const float* bfrag, int dtype, int out_mode,
+hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const void* bfrag, int dtype, int out_mode,
                           hipStream_t s) {
     auto go = [&](auto outt) {
         using OutT = decltype(outt);
