@@ -284,6 +284,16 @@ template <int SPS> struct TxMfmaCfg {
     static constexpr int NCOP = SB % 4 == 0 ? 1 : 4 / SB;   // plane copies (8-B aligned A reads)
 };
 
+// Carrier mix of one sample, packed: (re, im) = (y*cs - yi*sn, y*sn + yi*cs), y = (yr, yi),
+// cssn = (cs, sn) straight from v_sin/v_cos (hence the wait state, see cmix in modem_rx.hip).
+__device__ __forceinline__ cf2 tx_cmix(cf2 y, cf2 cssn) {
+    cf2 t, z;
+    asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(y), "v"(cssn));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]"
+        : "=v"(z) : "v"(y), "v"(cssn), "v"(t));
+    return z;
+}
+
 typedef _Float16 th8 __attribute__((ext_vector_type(8)));
 typedef _Float16 th4 __attribute__((ext_vector_type(4)));
 
@@ -347,7 +357,10 @@ struct TxMfma {
         const int i = lane & 15, g = lane >> 4;
         const int blk = (wave * SUB + q) * 16 + i;                  // row-block in the tile
         const int cp = ((4 - ((blk * SB) & 3)) & 3) / (SB < 4 ? SB : 4);   // copy shifting the row to 8 B
-        const _Float16* ar = pl + (NCOP > 1 ? cp : 0) * 4 * PLN + blk * SB + (NCOP > 1 ? cp * SB : 0) + 8 * g;
+        // opaque lane offset: every plane / k-step read is this base + a non-negative immediate
+        int aoff = (NCOP > 1 ? cp : 0) * 4 * PLN + blk * SB + (NCOP > 1 ? cp * SB : 0) + 8 * g;
+        asm volatile("" : "+v"(aoff));
+        const _Float16* ar = pl + aoff;
         typedef _Float16 tq4 __attribute__((ext_vector_type(4), aligned(8)));
         auto ld8 = [](const _Float16* a) {                          // 8-B aligned 16-B read
             const tq4 x = *reinterpret_cast<const tq4*>(a), y = *reinterpret_cast<const tq4*>(a + 4);
@@ -359,7 +372,7 @@ struct TxMfma {
         dim = (f32x4){(float)bh[0][0], 0.f, 0.f, 0.f};
         return;
 #endif
-        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, r1 = r0, m0 = r0, m1 = r0;
+        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;     // one accumulator per rail
         th8 a[2][4];
         auto load = [&](int s, int slot) {
             a[slot][0] = ld8(ar + 32 * s);
@@ -374,63 +387,71 @@ struct TxMfma {
             if (s + 1 < NKS) load(s + 1, c ^ 1);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bh[s], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bh[s], m0, 0, 0, 0);
-            r1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bl[s], r1, 0, 0, 0);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bl[s], m1, 0, 0, 0);
-            r1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], bh[s], r1, 0, 0, 0);
-            m1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], bh[s], m1, 0, 0, 0);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bl[s], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bl[s], m0, 0, 0, 0);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], bh[s], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], bh[s], m0, 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
-        dre = r0 + r1;
-        dim = m0 + m1;
+        dre = r0;
+        dim = m0;
     }
 
     // Full 16x16 tile, carrier index < 2^32: unconditional stores. jt = call sample index of
-    // the sub-tile's first sample.
-    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, int kab) {
+    // the sub-tile's first sample. Per sample: packed unscale (2^-kab), bit-exact phase,
+    // sin/cos, packed mix; stores through a uniform base + 32-bit lane offsets.
+    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
         const int lane = threadIdx.x & 63;
-        const uint32_t nb = (uint32_t)(p.s0 + (uint64_t)jt);
-        float zr[4], zi[4];
+        int loff = 64 * (lane >> 4) + (lane & 15);          // sample of row r: loff + 16 r
+        asm volatile("" : "+v"(loff));
+        const uint32_t nb = (uint32_t)(p.s0 + (uint64_t)jt) + (uint32_t)loff;
+        cf2 z[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
-            const float yr = __builtin_ldexpf(dre[r], -kab), yi = __builtin_ldexpf(dim[r], -kab);
-            zr[r] = yr;
-            zi[r] = yi;
-#ifdef MODEM_ABLATE_MIX
-            if (false) {
-#else
+            z[r] = (cf2){dre[r], dim[r]} * unscale;
+#ifndef MODEM_ABLATE_MIX
             if (OUT_MODE != OUT_IQ_BASEBAND) {
-#endif
                 float sn, cs;
-                sincos_phase(phase_from_f(p.w, (float)(nb + (uint32_t)off)), sn, cs);
-                zr[r] = __builtin_fmaf(yr, cs, -(yi * sn));
-                zi[r] = __builtin_fmaf(yr, sn, yi * cs);
+                sincos_phase(phase_from_f(p.w, (float)(nb + (uint32_t)(16 * r))), sn, cs);
+                z[r] = tx_cmix(z[r], (cf2){cs, sn});
             }
+#endif
         }
 #ifdef MODEM_ABLATE_STORE
 #pragma unroll
-        for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(zr[r]), "v"(zi[r]));
+        for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(z[r]));
 #else
-        OutT* ob = reinterpret_cast<OutT*>(p.out) + (OUT_MODE == OUT_REAL ? 1 : 2) * jt;
+        // wave-uniform base in SGPRs + 32-bit lane byte offsets (saddr + voffset stores)
+        constexpr int SBYTES = (OUT_MODE == OUT_REAL ? 1 : 2) * (int)sizeof(OutT);
+        const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
+        char* ob = reinterpret_cast<char*>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(oa >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)oa));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const uint32_t off = (uint32_t)(16 * (4 * (lane >> 4) + r) + (lane & 15));
-            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(ob, off, zr[r]);
-            else OutIO<OutT>::store_one(ob, off, zr[r], zi[r]);
+            char* q = ob + (uint32_t)((loff + 16 * r) * SBYTES);
+            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(q, 0, z[r].x);
+            else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
         }
 #endif
     }
 
-    // Partial tile, samples before the call, or carrier index >= 2^32: guarded.
-    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, int kab) {
+    // Partial tile, samples before the call, or carrier index >= 2^32: guarded, 64-bit
+    // indices; the same arithmetic as emit_full (a sample's bits never depend on the path).
+    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
         const int lane = threadIdx.x & 63;
         const int64_t jend = p.nsym * SPS;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
-            if (jt + off >= 0 && jt + off < jend)
-                tx_emit_off<OUT_MODE, OutT>(p, jt, off, make_float2(__builtin_ldexpf(dre[r], -kab),
-                                            __builtin_ldexpf(dim[r], -kab)), make_float2(0.f, 0.f), false);
+            if (jt + off < 0 || jt + off >= jend) continue;
+            cf2 z = (cf2){dre[r], dim[r]} * unscale;
+            if (OUT_MODE != OUT_IQ_BASEBAND) {
+                float sn, cs;
+                sincos_phase(carrier_phase_off(p.w, p.s0 + (uint64_t)jt, off, p.small_n), sn, cs);
+                z = tx_cmix(z, (cf2){cs, sn});
+            }
+            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, jt + off, z.x);
+            else OutIO<OutT>::store_one(p.out, jt + off, z.x, z.y);
         }
     }
 
@@ -442,6 +463,8 @@ struct TxMfma {
         const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int lead = p.lead;
         const int kab = p.lut_scale_exp + p.tap_scale_exp;
+        const float us = __builtin_ldexpf(1.0f, -kab);             // exact (|kab| < 126)
+        const cf2 unscale = {us, us};
         const int64_t mlast = p.nsym_valid - 1;
         // full tile: every staged symbol is data of this call, every sample is emitted
         auto full = [&](int64_t t) {
@@ -475,7 +498,7 @@ struct TxMfma {
                     for (int q = 0; q < SUB; ++q) {
                         f32x4 dre, dim;
                         fir(pl, q, bh, bl, dre, dim);
-                        emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, kab);
+                        emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                     }
                     __syncthreads();                     // the window is restaged next trip
                 }
@@ -487,7 +510,7 @@ struct TxMfma {
                 for (int q = 0; q < SUB; ++q) {
                     f32x4 dre, dim;
                     fir(pl, q, bh, bl, dre, dim);
-                    emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, kab);
+                    emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                 }
                 __syncthreads();
                 ++t;
