@@ -95,7 +95,13 @@ int rx_mfma_ksteps(int decim, int L);
 constexpr int rx_mfma_table_copies(int decim) {
     return 8 / (decim % 8 == 0 ? 8 : decim % 4 == 0 ? 4 : decim % 2 == 0 ? 2 : 1);
 }
-constexpr int rx_mfma_table_len(int decim, int nks) { return (32 * nks + 15 * decim + 8 + 7) & ~7; }
+// Padded so that a copy's hi + lo (4 * len bytes) is 64 B past a multiple of 256: the NC
+// copies then start in disjoint LDS bank groups (the 8 lanes of one ds_read_b128 cycle hit
+// distinct banks).
+constexpr int rx_mfma_table_len(int decim, int nks) {
+    const int n = (32 * nks + 15 * decim + 8 + 7) & ~7;
+    return n + ((16 - (n % 64)) % 64 + 64) % 64;   // n % 64 == 16 -> 4n % 256 == 64
+}
 hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const void* tables, int in_dtype,
                           int out_dtype, int mix, hipStream_t s);
 hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,

@@ -467,7 +467,7 @@ struct RxMfma {
             for (int j = 0; j < 4; ++j) {
                 float sn, cs;
 #ifdef MODEM_ABLATE_MIX
-                sn = 0.f; cs = (float)(lb + (uint32_t)(4 * NT * u + j));
+                sn = 0.f; cs = __uint_as_float(0x3f000000u | ((lb + (uint32_t)(4 * NT * u + j)) & 0xffu));
 #else
                 sincos_phase(phase_from_f(p.w, (float)(lb + (uint32_t)(4 * NT * u + j))), sn, cs);
 #endif
@@ -621,7 +621,7 @@ struct RxMfma {
                 int e0 = l0 + 4 * NT * u;
                 if ((u + 1) * NT > NQ) e0 = e0 < 4 * (NQ - 1) ? e0 : 4 * (NQ - 1);   // spare lanes
 #ifdef MODEM_ABLATE_LOAD
-                float v = (float)(base + e0);
+                float v = 0.5f + 1e-3f * (float)(e0 & 7);   // in the f16 window: no restaging
                 asm volatile("" : "+v"(v));
                 if constexpr (std::is_same<InT, float>::value) pre[u] = QT{make_float4(v, v, v, v), make_float4(v, v, v, v)};
                 else pre[u] = make_uint4(__float_as_uint(v), 0, 0, 0);
@@ -639,7 +639,7 @@ struct RxMfma {
                     const int64_t n_lo = q_lo_of(p, t) + p.n_start;
                     const int ka = stage_fast(p, pl, red, (uint32_t)(p.c0 + (uint64_t)n_lo), pre);
                     if (ka != 0) { restage = true; break; }       // uniform; leaves the loop
-                    __syncthreads();
+                    // (the tile-max reduction in stage_fast ended with a barrier: planes visible)
                     if (t + 1 < t1) prefetch(t + 1);       // next samples fly during the MFMAs
                     f32x4 dre, dim;
                     fir(pl, tbl, dre, dim);
