@@ -297,6 +297,8 @@ struct modem_tx {
     float* d_bfrag = nullptr;       // its split-f16 per-lane B fragments (modem_internal.h)
     float* d_luth = nullptr;        // its split-f16 LUT (re_hi, re_lo, im_hi, im_lo per entry)
     int lut_scale_exp = 0, tap_scale_exp = 0;
+    int levels = 0;                 // integer-level LUT (see TxParams)
+    float level_inv = 0.0f;
     uint64_t symbols = 0;           // symbols emitted so far (row-block alignment)
     Stage bits_stage, out_stage;
     ~modem_tx() {
@@ -364,19 +366,42 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
         // Split-f16 operands of tx_mfma (modem_tx.hip). Exact power-of-two scales put the
         // maxima of the LUT and of the taps in [2^14, 2^15); both are split hi + lo =
         // rn_f16(v) + rn_f16(v - hi).
-        auto scale_exp = [](float mx) {
+        auto scale_exp = [](float mx) {   // 0 inside [2^-3, 2^15), else into [2^14, 2^15)
             int e = 0;
-            if (mx > 0.0f && std::isfinite(mx)) { std::frexp(mx, &e); return 15 - e; }
-            return 0;
+            if (!(mx > 0.0f) || !std::isfinite(mx) || (mx >= 0.125f && mx < 32768.0f)) return 0;
+            std::frexp(mx, &e);
+            return 15 - e;
         };
         auto split = [](float v, _Float16& hi, _Float16& lo) { hi = (_Float16)v; lo = (_Float16)(v - (float)hi); };
         float lmax = 0.0f, tmax = 0.0f;
         for (size_t k = 0; k < 2 * nl; ++k) lmax = std::max(lmax, std::fabs(d->lut[k]));
         for (uint32_t k = 0; k < d->ntaps; ++k) tmax = std::max(tmax, std::fabs(d->taps[k]));
-        h->lut_scale_exp = scale_exp(lmax);
+        // Integer levels: every component v = q * s, q an integer with |q| <= 2048 (exact f16),
+        // s the smallest nonzero |component|. Then A = q exactly and s moves into the taps.
+        double smin = 0.0;
+        for (size_t k = 0; k < 2 * nl; ++k) {
+            const double a = std::fabs((double)d->lut[k]);
+            if (a > 0.0 && (smin == 0.0 || a < smin)) smin = a;
+        }
+        bool levels = smin > 0.0;
+        for (size_t k = 0; levels && k < 2 * nl; ++k) {
+            const double q = (double)d->lut[k] / smin, r = std::nearbyint(q);
+            levels = std::fabs(r) <= 2048.0 && std::fabs(q - r) <= 1e-6 * std::max(1.0, std::fabs(q));
+        }
+        h->levels = levels ? 1 : 0;
+        h->level_inv = levels ? (float)(1.0 / smin) : 0.0f;
+        const double tscale = levels ? smin : 1.0;           // folded into the taps
+        tmax = (float)(tmax * tscale);
+        h->lut_scale_exp = levels ? 0 : scale_exp(lmax);
         h->tap_scale_exp = scale_exp(tmax);
         std::vector<_Float16> lh(4 * nl);
         for (size_t k = 0; k < nl; ++k) {
+            if (levels) {
+                lh[4 * k] = (_Float16)std::nearbyint((double)d->lut[2 * k] / smin);
+                lh[4 * k + 2] = (_Float16)std::nearbyint((double)d->lut[2 * k + 1] / smin);
+                lh[4 * k + 1] = lh[4 * k + 3] = (_Float16)0.0f;
+                continue;
+            }
             split(std::ldexp(d->lut[2 * k], h->lut_scale_exp), lh[4 * k], lh[4 * k + 1]);
             split(std::ldexp(d->lut[2 * k + 1], h->lut_scale_exp), lh[4 * k + 2], lh[4 * k + 3]);
         }
@@ -389,7 +414,8 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
                 for (int jj = 0; jj < 8; ++jj) {
                     const int o = 32 * s2 + 8 * (l >> 4) + jj, j = l & 15, c = j / sps, ph = j % sps;
                     const int t = c + PRE - o;
-                    const float v = (t >= 0 && t < (int)h->K) ? std::ldexp(pp[(size_t)t * sps + ph], h->tap_scale_exp) : 0.0f;
+                    const float v = (t >= 0 && t < (int)h->K)
+                        ? std::ldexp((float)((double)pp[(size_t)t * sps + ph] * tscale), h->tap_scale_exp) : 0.0f;
                     split(v, bf[(((size_t)s2 * 2) * 64 + l) * 8 + jj], bf[(((size_t)s2 * 2 + 1) * 64 + l) * 8 + jj]);
                 }
         const size_t nb = (bf.size() * sizeof(_Float16) + sizeof(float) - 1) / sizeof(float);
@@ -458,6 +484,8 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     p.lut_h = h->d_luth;
     p.lut_scale_exp = h->lut_scale_exp;
     p.tap_scale_exp = h->tap_scale_exp;
+    p.levels = h->levels;
+    p.level_inv = h->level_inv;
     const uint32_t sb = (h->sps <= 16 && 16 % h->sps == 0) ? 16 / h->sps : 1;   // symbols per row-block
     p.lead = (int)(h->symbols % sb);
     if (h->mfma_ksteps > 0)
@@ -575,15 +603,19 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
     h->mfma_ksteps = force_valu ? 0 : mk::rx_mfma_ksteps((int)h->decim, (int)h->ntaps);
     if (h->mfma_ksteps > 0) {
         // Split-f16 tap tables of rx_mfma (modem_rx.hip): the reversed taps T[x] = h[W-1-x]
-        // scaled by 2^kb (max |h| * 2^kb in [2^14, 2^15): exact, keeps f16 in range), as f16
+        // scaled by 2^kb (exact; 0 when max |h| is in [2^-3, 2^15), else into [2^14, 2^15)), as f16
         // hi then lo = rn_f16(v - hi), in NC copies shifted by gcd(decim, 8) so that every
         // lane's 8-tap read is 16-B aligned.
         const int nks = h->mfma_ksteps, W = 32 * nks, dec = (int)h->decim;
         const int nc = mk::rx_mfma_table_copies(dec), tb = mk::rx_mfma_table_len(dec, nks), gq = 8 / nc;
         float hmax = 0.0f;
         for (uint32_t k = 0; k < h->ntaps; ++k) hmax = std::max(hmax, std::fabs(d->taps[k]));
-        int kb = 0;
-        if (hmax > 0.0f && std::isfinite(hmax)) { int e; std::frexp(hmax, &e); kb = 15 - e; }
+        int kb = 0;   // 0 inside [2^-3, 2^15), else into [2^14, 2^15)
+        if (hmax > 0.0f && std::isfinite(hmax) && !(hmax >= 0.125f && hmax < 32768.0f)) {
+            int e;
+            std::frexp(hmax, &e);
+            kb = 15 - e;
+        }
         h->tap_scale_exp = kb;
         std::vector<_Float16> tab((size_t)nc * 2 * tb, (_Float16)0.0f);
         for (int c = 0; c < nc; ++c)

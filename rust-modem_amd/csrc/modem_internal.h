@@ -36,6 +36,11 @@ struct TxParams {
     int32_t lut_scale_exp;
     int32_t tap_scale_exp;
     int32_t lead;
+    // levels: every LUT component is an integer multiple of one scale s, folded into the taps;
+    // lut_h then holds the exact f16 integer levels (lo halves zero) and a symbol value v of the
+    // history maps to the level rint(v * level_inv), level_inv = 1/s.
+    int32_t levels;
+    float level_inv;
 };
 
 // One RX launch: input samples [0, N) (stream indices n_start ..), outputs k_first ..

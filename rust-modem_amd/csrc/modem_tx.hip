@@ -271,8 +271,10 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
 // As on the RX, every operand is split in two f16 halves (a = a_hi + a_lo, round to nearest)
 // and A*B ~= A_hi*B_hi + A_hi*B_lo + A_lo*B_hi accumulates in f32 (6 MFMAs per k-step for the
 // re and im rails). The LUT and the taps are scaled by exact powers of two on the host
-// (2^lut_scale_exp, 2^tap_scale_exp: maxima in [2^14, 2^15)), split there, and the outputs
-// are scaled back with ldexp. Row-blocks are aligned to the absolute symbol index
+// (2^lut_scale_exp, 2^tap_scale_exp; 0 when the maxima already lie in [2^-3, 2^15), else into
+// [2^14, 2^15)), split there, and the outputs are scaled back. When every LUT component is an
+// integer multiple of one scale s (QAM, BPSK at pi/4, QPSK at 0, BASK) the symbols are the
+// exact f16 integer levels, s is folded into the taps and the A_lo products vanish. Row-blocks are aligned to the absolute symbol index
 // (lead = symbols before this call, mod SB), so a symbol always meets the same taps at the
 // same k positions and a stream cut into calls gives the same samples as one call.
 // Sample-and-hold (no taps) stays on the exact VALU kernels.
@@ -333,8 +335,11 @@ struct TxMfma {
 
     // f32 symbol value -> scaled (2^ka) split halves (re_hi, re_lo, im_hi, im_lo), as the host
     // splits the LUT (round to nearest both times).
-    __device__ static th4 split_value(float2 v, int ka) {
-        const float r = __builtin_ldexpf(v.x, ka), i = __builtin_ldexpf(v.y, ka);
+    __device__ static th4 split_value(const TxParams& p, float2 v) {
+        if (p.levels)      // the exact integer level of a history symbol (lo halves zero)
+            return (th4){(_Float16)__builtin_rintf(v.x * p.level_inv), (_Float16)0.0f,
+                         (_Float16)__builtin_rintf(v.y * p.level_inv), (_Float16)0.0f};
+        const float r = __builtin_ldexpf(v.x, p.lut_scale_exp), i = __builtin_ldexpf(v.y, p.lut_scale_exp);
         const _Float16 rh = (_Float16)r, ih = (_Float16)i;
         return (th4){rh, (_Float16)(r - (float)rh), ih, (_Float16)(i - (float)ih)};
     }
@@ -346,11 +351,13 @@ struct TxMfma {
             float2 v;
             if (m < 0) v = m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f);
             else v = m >= p.nsym_valid ? make_float2(0.f, 0.f) : p.lut[tx_symbol_index(p, m)];
-            put(pl, e, split_value(v, p.lut_scale_exp));
+            put(pl, e, split_value(p, v));
         }
     }
 
     // 16x16 sub-tile q of this wave: D = sum over the window of A*B (split products).
+    // LV: integer-level symbols (exact f16, no lo plane): 2 MFMAs per rail and k-step, else 3.
+    template <bool LV>
     __device__ static void fir(const _Float16* pl, int q, const th8 (&bh)[NKS], const th8 (&bl)[NKS],
                                f32x4& dre, f32x4& dim) {
         const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -376,9 +383,9 @@ struct TxMfma {
         th8 a[2][4];
         auto load = [&](int s, int slot) {
             a[slot][0] = ld8(ar + 32 * s);
-            a[slot][1] = ld8(ar + PLN + 32 * s);
+            if (!LV) a[slot][1] = ld8(ar + PLN + 32 * s);
             a[slot][2] = ld8(ar + 2 * PLN + 32 * s);
-            a[slot][3] = ld8(ar + 3 * PLN + 32 * s);
+            if (!LV) a[slot][3] = ld8(ar + 3 * PLN + 32 * s);
         };
         load(0, 0);
 #pragma unroll
@@ -389,8 +396,10 @@ struct TxMfma {
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bh[s], m0, 0, 0, 0);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bl[s], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bl[s], m0, 0, 0, 0);
-            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], bh[s], r0, 0, 0, 0);
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], bh[s], m0, 0, 0, 0);
+            if (!LV) {
+                r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], bh[s], r0, 0, 0, 0);
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], bh[s], m0, 0, 0, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
         dre = r0;
@@ -407,8 +416,13 @@ struct TxMfma {
         const uint32_t nb = (uint32_t)(p.s0 + (uint64_t)jt) + (uint32_t)loff;
         cf2 z[4];
 #pragma unroll
+        for (int r = 0; r < 4; ++r) z[r] = (cf2){dre[r], dim[r]};
+        if (unscale.x != 1.0f) {                            // uniform; scale 1 is the usual case
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[r] *= unscale;
+        }
+#pragma unroll
         for (int r = 0; r < 4; ++r) {
-            z[r] = (cf2){dre[r], dim[r]} * unscale;
 #ifndef MODEM_ABLATE_MIX
             if (OUT_MODE != OUT_IQ_BASEBAND) {
                 float sn, cs;
@@ -463,6 +477,7 @@ struct TxMfma {
         const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int lead = p.lead;
         const int kab = p.lut_scale_exp + p.tap_scale_exp;
+        const bool lv = p.levels != 0;
         const float us = __builtin_ldexpf(1.0f, -kab);             // exact (|kab| < 126)
         const cf2 unscale = {us, us};
         const int64_t mlast = p.nsym_valid - 1;
@@ -497,7 +512,8 @@ struct TxMfma {
 #pragma unroll
                     for (int q = 0; q < SUB; ++q) {
                         f32x4 dre, dim;
-                        fir(pl, q, bh, bl, dre, dim);
+                        if (lv) fir<true>(pl, q, bh, bl, dre, dim);
+                        else fir<false>(pl, q, bh, bl, dre, dim);
                         emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                     }
                     __syncthreads();                     // the window is restaged next trip
@@ -509,7 +525,8 @@ struct TxMfma {
 #pragma unroll 1
                 for (int q = 0; q < SUB; ++q) {
                     f32x4 dre, dim;
-                    fir(pl, q, bh, bl, dre, dim);
+                    if (lv) fir<true>(pl, q, bh, bl, dre, dim);
+                    else fir<false>(pl, q, bh, bl, dre, dim);
                     emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                 }
                 __syncthreads();

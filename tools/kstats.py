@@ -17,4 +17,7 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    try:
+        main(sys.argv[1])
+    except BrokenPipeError:      # `| head` closed the pipe
+        pass

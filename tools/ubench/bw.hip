@@ -22,6 +22,25 @@ __global__ void rd4(const float4* x, float* o) {
   }
   if (a.x == 12345.f) o[0] = a.y + a.z + a.w;
 }
+// Each lane reads 32 contiguous bytes as two 16-B loads (lane stride 32 B), the RX quad pattern.
+__global__ void rd8(const float4* x, float* o) {
+  float4 a = {0, 0, 0, 0};
+  for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; 2 * i < N4; i += gridDim.x * blockDim.x) {
+    float4 v = x[2 * i], w = x[2 * i + 1];
+    a.x += v.x + w.x; a.y += v.y + w.y; a.z += v.z + w.z; a.w += v.w + w.w;
+  }
+  if (a.x == 12345.f) o[0] = a.y + a.z + a.w;
+}
+// The same bytes with both loads coalesced (lane stride 16 B, second load 1 block later).
+__global__ void rd8c(const float4* x, float* o) {
+  float4 a = {0, 0, 0, 0};
+  const size_t step = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * 2 * (size_t)blockDim.x + threadIdx.x; i < N4; i += 2 * step) {
+    float4 v = x[i], w = x[i + blockDim.x];
+    a.x += v.x + w.x; a.y += v.y + w.y; a.z += v.z + w.z; a.w += v.w + w.w;
+  }
+  if (a.x == 12345.f) o[0] = a.y + a.z + a.w;
+}
 __global__ void cp4(const float4* x, float4* o) {
   for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N4; i += gridDim.x * blockDim.x) o[i] = x[i];
 }
@@ -45,6 +64,8 @@ int main() {
     snprintf(n, 64, "write float4 nt grid=%d", g); run(n, B, [&] { hipLaunchKernelGGL(wr4nt, g, 256, 0, 0, y, 1.f); });
     snprintf(n, 64, "write float2 grid=%d", g); run(n, B, [&] { hipLaunchKernelGGL(wr2, g, 256, 0, 0, (float2*)y, 1.f); });
     snprintf(n, 64, "read float4 grid=%d", g); run(n, B, [&] { hipLaunchKernelGGL(rd4, g, 256, 0, 0, x, o); });
+    snprintf(n, 64, "read 2xfloat4/lane stride32 g=%d", g); run(n, B, [&] { hipLaunchKernelGGL(rd8, g, 256, 0, 0, x, o); });
+    snprintf(n, 64, "read 2xfloat4 coalesced g=%d", g); run(n, B, [&] { hipLaunchKernelGGL(rd8c, g, 256, 0, 0, x, o); });
     snprintf(n, 64, "copy float4 grid=%d", g); run(n, 2 * B, [&] { hipLaunchKernelGGL(cp4, g, 256, 0, 0, x, y); });
   }
   // write 128 MB then read it back (TX -> RX through the sample buffer): is the re-read L3-served?
