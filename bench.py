@@ -108,9 +108,15 @@ class GpuRunner:
         self.torch.cuda.synchronize()
 
     def kernel_times_ms(self, reps):
-        """Mean device time of the TX and RX launches, HIP events on the launch stream."""
+        """Mean device time of the TX and RX launches, HIP events on the launch stream.
+
+        Untimed steps are queued first so that the device has a backlog: events recorded
+        while it waits for the host would time the host's enqueue rate, not the kernels."""
         torch = self.torch
         ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(reps)]
+        for _ in range(16):
+            self.tx(0)
+            self.rx(0)
         for r in range(reps):
             ev[r][0].record(self.stream)
             self.tx(0)

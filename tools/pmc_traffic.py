@@ -21,7 +21,8 @@ def main(d, config, path):
     entry = {"unit": "bytes per launch", "source": d,
              "correction": "2 x FETCH_SIZE (KiB) + WRITE_SIZE (KiB), x1024"}
     for k, cs in res.items():
-        kind = "tx" if k.startswith("tx_") else "rx" if k.startswith("rx_") else None
+        # names may come demangled ("tx_mfma<...>") or mangled ("_ZN2mk7tx_mfma...")
+        kind = "tx" if ("tx_mfma" in k or "tx_fast" in k) else "rx" if ("rx_mfma" in k or "rx_fast" in k) else None
         if kind and "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             entry[kind] = int(round((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024))
             entry[kind + "_kernel"] = k
