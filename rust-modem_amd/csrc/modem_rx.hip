@@ -474,9 +474,12 @@ struct RxMfma {
         uint32_t lb = nb32 + 4u * (uint32_t)tid;
         int pos0 = rxh_pos(4 * tid, RW);                  // slot u writes at pos0 + u * SLOT_POS
         asm volatile("" : "+v"(lb), "+v"(pos0));
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         float mx = 0.f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+            // the last slot is partial: only the waves that own some of its quads run it
+            if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) continue;   // wave-uniform
             float2 x[4];
             Q::split(pre[u], x);
             const int e0 = 4 * (tid + NT * u);
@@ -641,7 +644,8 @@ struct RxMfma {
             int l0 = 4 * tid;                               // opaque: no per-slot hoisted addresses
             asm volatile("" : "+v"(l0));
 #pragma unroll
-            for (int u = 0; u < U; ++u) pre[u] = load_slot(p, base, l0, u);
+            for (int u = 0; u < U; ++u)                     // the partial last slot: its waves only
+                if ((u + 1) * NT <= NQ || 64 * wave + NT * u < NQ) pre[u] = load_slot(p, base, l0, u);
         };
         int64_t t = t0;
         bool restage = false;
@@ -690,6 +694,14 @@ __global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const _Float16*
     const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;
     const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
     if (t0 >= t1) return;
+#ifdef MODEM_STAGGER
+    // workgroups dealt to the same CU (b, b + CUs, ...) start a fraction of a tile apart so
+    // their staging (VALU) and matrix phases interleave instead of running in lockstep
+    {
+        const int k = (int)(blockIdx.x / (unsigned)MODEM_STAGGER) % 3;
+        for (int i = 0; i < k * 12; ++i) __builtin_amdgcn_s_sleep(127);   // ~8K cycles each step
+    }
+#endif
     // f32 input with the complex mix (the loopback chain): the epilogue is specialised on what
     // it stores, so the tile loop's store count is static. Other variants share the guarded one.
     if (std::is_same<InT, float>::value && MIX == MIX_COMPLEX) {
