@@ -108,25 +108,32 @@ class GpuRunner:
         self.torch.cuda.synchronize()
 
     def kernel_times_ms(self, reps):
-        """Mean device time of the TX and RX launches, HIP events on the launch stream.
+        """Mean device time of the TX and RX launches, from HIP events on the launch stream.
 
-        Untimed steps are queued first so that the device has a backlog: events recorded
-        while it waits for the host would time the host's enqueue rate, not the kernels."""
+        Events between every pair of kernels add their own gaps, so the chain is timed as
+        `reps` back-to-back TX+RX steps between two events, TX alone as `reps` back-to-back TX
+        launches, and RX as the difference. Untimed steps are queued first so that the device
+        has a backlog (events recorded while it waits for the host would time the host)."""
         torch = self.torch
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(reps)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         for _ in range(16):
             self.tx(0)
             self.rx(0)
-        for r in range(reps):
-            ev[r][0].record(self.stream)
+        ev[0].record(self.stream)
+        for _ in range(reps):
             self.tx(0)
-            ev[r][1].record(self.stream)
             self.rx(0)
-            ev[r][2].record(self.stream)
+        ev[1].record(self.stream)
+        for _ in range(8):
+            self.tx(0)
+        ev[2].record(self.stream)
+        for _ in range(reps):
+            self.tx(0)
+        ev[3].record(self.stream)
         torch.cuda.synchronize()
-        t_tx = float(np.mean([ev[r][0].elapsed_time(ev[r][1]) for r in range(reps)]))
-        t_rx = float(np.mean([ev[r][1].elapsed_time(ev[r][2]) for r in range(reps)]))
-        return t_tx, t_rx
+        t_chain = ev[0].elapsed_time(ev[1]) / reps
+        t_tx = ev[2].elapsed_time(ev[3]) / reps
+        return t_tx, t_chain - t_tx
 
     def check(self):
         """Decisions of channel 0 equal the symbols sent (size-independent parity property)."""

@@ -6,6 +6,7 @@
 
 #include <hip/hip_fp16.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -169,8 +170,18 @@ static inline int resident_blocks(const void* kernel, int threads, size_t lds) {
     return occ;
 }
 
-static inline unsigned persistent_grid(const void* kernel, int threads, size_t lds, int64_t ntiles) {
-    const int64_t cap = (int64_t)resident_blocks(kernel, threads, lds) * device_cus();
+// Optional cap on workgroups per CU (0 = occupancy limit), e.g. to leave room for a kernel of
+// another stream that runs concurrently (experiments: MODEM_TX_WGS_PER_CU / MODEM_RX_WGS_PER_CU).
+static inline int env_wgs_per_cu(const char* name) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : 0;
+}
+
+static inline unsigned persistent_grid(const void* kernel, int threads, size_t lds, int64_t ntiles,
+                                       int cap_per_cu = 0) {
+    int per_cu = resident_blocks(kernel, threads, lds);
+    if (cap_per_cu > 0 && cap_per_cu < per_cu) per_cu = cap_per_cu;
+    const int64_t cap = (int64_t)per_cu * device_cus();
     const int64_t g = ntiles < cap ? ntiles : cap;
     return (unsigned)(g > 0 ? g : 1);
 }
@@ -231,5 +242,34 @@ __device__ __forceinline__ void mfma_chain_lb(const float2* arow, OffF off, cons
     }
 }
 
+
+// ------------------------------------------------------------- diagnostic stamps ----
+// MODEM_STAMPS builds only (tools/stamps.py): per-wave cycle sums of a tile loop's segments,
+// accumulated in scalar registers and stored once by lane 0 into g_stamps (a buffer no other
+// code reads). Never compiled into the product library.
+#ifdef MODEM_STAMPS
+constexpr int kStampSegs = 12;   // 8 segment sums, then realtime at entry / exit, spare
+static __device__ unsigned long long g_stamps[4096 * 4 * kStampSegs];
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+__device__ __forceinline__ unsigned long long stamp_real() {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+    return t;
+}
+#define STAMP_DECL unsigned long long st_sum[kStampSegs] = {0}, st_last = stamp_now(); st_sum[8] = stamp_real()
+#define STAMP(k) do { const unsigned long long t_ = stamp_now(); st_sum[k] += t_ - st_last; st_last = t_; } while (0)
+#define STAMP_FLUSH(slot) do { st_sum[9] = stamp_real(); if ((threadIdx.x & 63) == 0) \
+    for (int k_ = 0; k_ < kStampSegs; ++k_) g_stamps[(size_t)(slot) * kStampSegs + k_] = st_sum[k_]; } while (0)
+#else
+#define STAMP_DECL do {} while (0)
+#define STAMP(k) do {} while (0)
+#define STAMP_FLUSH(slot) do {} while (0)
+#endif
 
 }  // namespace mk

@@ -307,17 +307,19 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
 // mixed samples of a tile are used as they are when the tile's max |z| lies in
 // [2^-3, 2^15) (results then never depend on how a stream is cut into calls), and scaled
 // by 2^ka into [2^14, 2^15) otherwise. Outputs are scaled back with ldexp (exact).
-// LDS: four f16 planes (re_hi, re_lo, im_hi, im_lo) in natural sample order with 8 pad
-// halves after every RW = 16*DEC samples (the 16 rows of a 16-B read hit distinct bank
-// groups), and NC shifted copies of the hi/lo reversed-tap table so that every lane's
+// LDS: four f16 planes (re_hi, re_lo, im_hi, im_lo) in natural sample order with 16 pad
+// halves after every RW = 16*DEC samples (rxh_pos: conflict-free 16-B A reads), and NC shifted copies of the hi/lo reversed-tap table so that every lane's
 // 8-tap B read is one aligned ds_read_b128.
-template <int DEC> struct RxMfmaCfg {
-    static constexpr int NT = 256;               // 4 waves
-    static constexpr int TS = 4 * 256;           // kept instants per workgroup tile
+template <int DEC, int NT_> struct RxMfmaCfg {
+    static constexpr int NT = NT_;               // 64 (one wave) or 256 (4 waves)
+    static constexpr int TS = NT / 64 * 256;     // kept instants per workgroup tile
     static constexpr int RW = 16 * DEC;          // samples per A row
-    static constexpr int RP = RW + 8;            // padded row pitch (halves)
+    static constexpr int RP = RW + 16;           // padded row pitch (halves)
 };
-__host__ __device__ constexpr int rxh_pos(int e, int RW) { return e + 8 * (e / RW); }
+// Plane position of staged sample e: 16 pad halves after every RW samples. With the row pitch
+// RW + 16 (= 2 mod 4 in 16-B units), the 16 lanes of each ds_read_b128 lane group (rows i at
+// k-offset g, rows i' at g + 1) hit distinct bank quads; a pitch of RW + 8 was 2-way conflicted.
+__host__ __device__ constexpr int rxh_pos(int e, int RW) { return e + 16 * (e / RW); }
 
 // What the steady-state epilogue writes: baseband IQ, QAM-axis decisions, or both
 // (RXE_GEN: any other combination, guarded per store).
@@ -392,20 +394,25 @@ __device__ __forceinline__ float wave_max(float m) {
 }
 
 // Tile scale exponent from the lanes' max |z| (one barrier; red: 4 floats of LDS).
+template <int NT>
 __device__ __forceinline__ int tile_scale_exp(float lane_max, float* red) {
-    const float wm = wave_max(lane_max);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wm;
-    __syncthreads();
-    const float m = __builtin_fmaxf(__builtin_fmaxf(red[0], red[1]), __builtin_fmaxf(red[2], red[3]));
+    float m = wave_max(lane_max);
+    if (NT == 64) {
+        __syncthreads();                                    // one wave: orders the LDS planes only
+    } else {
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+        __syncthreads();
+        m = __builtin_fmaxf(__builtin_fmaxf(red[0], red[1]), __builtin_fmaxf(red[2], red[3]));
+    }
     const int ex = (int)((__float_as_uint(m) >> 23) & 0xff);
     if (ex >= 127 - 3 && ex < 127 + 15) return 0;          // max in [2^-3, 2^15): as is
     if (ex == 0 || ex == 0xff) return 0;                    // all zero / non-finite
     return 141 - ex;                                        // max * 2^k in [2^14, 2^15)
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NTT>
 struct RxMfma {
-    using C = RxMfmaCfg<DEC>;
+    using C = RxMfmaCfg<DEC, NTT>;
     using Q = Quad<InT>;
     using QT = typename Q::T;
     static constexpr int NT = C::NT, TS = C::TS, RW = C::RW, RP = C::RP;
@@ -416,10 +423,10 @@ struct RxMfma {
     static constexpr int PL = (rxh_pos(4 * NQ - 1, RW) + 1 + 7) & ~7;   // halves per plane
     static constexpr int NC = rx_mfma_table_copies(DEC);
     static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
-    static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 16;
+    static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 16;   // + red
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
     static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
-    static constexpr int SLOT_POS = 4 * NT + 8 * (4 * NT / RW);   // plane offset between slots
+    static constexpr int SLOT_POS = 4 * NT + 16 * (4 * NT / RW);  // plane offset between slots
 
     // Rows hold 16 instants aligned to the absolute instant index (k % 16 == column), so an
     // instant's taps always fall at the same k positions of the 32-wide MFMA sums and the
@@ -501,11 +508,20 @@ struct RxMfma {
                 if ((u + 1) * 4 * NT <= NS || e0 + j < NS)      // one v_max3 per sample
                     asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j]), "v"(zi[j]));
             }
+#ifdef MODEM_ABLATE_PUT
+            asm volatile("" :: "v"(zr[0]), "v"(zr[1]), "v"(zr[2]), "v"(zr[3]), "v"(zi[0]), "v"(zi[1]), "v"(zi[2]), "v"(zi[3]));
+#else
             if ((u + 1) * 4 * NT <= NS || e0 < NS) put4o(pl, pos0 + u * SLOT_POS, zr, zi, 1.0f);
+#endif
             __builtin_amdgcn_sched_barrier(0);              // one quad's temporaries at a time
         }
         // ka != 0 (rare: out-of-window magnitudes): the caller restages the tile scaled
-        return tile_scale_exp(mx, red);
+#ifdef MODEM_ABLATE_TMAX
+        asm volatile("" :: "v"(mx));
+        __syncthreads();
+        return 0;
+#endif
+        return tile_scale_exp<NT>(mx, red);
     }
 
     // First / last tiles of a chunk, unaligned input, carrier index >= 2^32: per sample, two
@@ -518,7 +534,7 @@ struct RxMfma {
                 const float2 z = rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j));
                 mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(z.x), __builtin_fabsf(z.y)));
             }
-        const int ka = tile_scale_exp(mx, red);
+        const int ka = tile_scale_exp<NT>(mx, red);
         const float sc = __builtin_ldexpf(1.0f, ka < -126 ? -126 : (ka > 127 ? 127 : ka));
         for (int e0 = 4 * threadIdx.x; e0 < NS; e0 += 4 * NT) {
             float zr[4], zi[4];
@@ -548,7 +564,7 @@ struct RxMfma {
         return;
 #endif
         f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;     // one accumulator per rail
-        auto aoff = [](int s) { return 32 * s + 8 * ((32 * s) / RW); };
+        auto aoff = [](int s) { return 32 * s + 16 * ((32 * s) / RW); };
         h8 a[2][4], b[2][2];
         auto load = [&](int s, int slot) {
             const int o = aoff(s);
@@ -615,10 +631,13 @@ struct RxMfma {
         }
     }
 
-    // Tiles of [t0, t1). When the input is 8-B aligned and the carrier indices stay below
-    // 2^32, the run of "full" tiles (all staged samples inside the chunk, all 1024 instants
-    // kept) goes through the prefetched loop, whose epilogue EM stores unconditionally; the
-    // first and last tiles of the chunk take the general path.
+    // Tiles of [t0, t1) (a contiguous range per workgroup: measured 9 % faster on C3 than
+    // handing neighbouring tiles to concurrently running workgroups, and dynamic tile handout
+    // through per-XCD atomic counters did not beat it either). When the input is 8-B aligned
+    // and the carrier indices stay below 2^32, the run of "full" tiles (all staged samples
+    // inside the chunk, all 1024 instants kept) goes through the prefetched loop, whose
+    // epilogue EM stores unconditionally; the first and last tiles of the chunk take the
+    // general path.
     template <int EM>
     __device__ static void run(const RxParams& p, _Float16* pl, const _Float16* tbl, float* red,
                                int64_t t0, int64_t t1) {
@@ -649,19 +668,30 @@ struct RxMfma {
         };
         int64_t t = t0;
         bool restage = false;
+        STAMP_DECL;
         while (t < t1) {
             if (full(t) && !restage) {
                 prefetch(t);
                 for (; t < t1 && full(t); ++t) {
                     const int64_t n_lo = q_lo_of(p, t) + p.n_start;
+#ifdef MODEM_STAMPS
+                    STAMP(0);                              // loop overhead
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    STAMP(1);                              // waiting for the tile's samples
+#endif
                     const int ka = stage_fast(p, pl, red, (uint32_t)(p.c0 + (uint64_t)n_lo), pre);
+                    STAMP(2);                              // staging + tile-max barrier
                     if (ka != 0) { restage = true; break; }       // uniform; leaves the loop
                     // (the tile-max reduction in stage_fast ended with a barrier: planes visible)
                     if (t + 1 < t1) prefetch(t + 1);       // next samples fly during the MFMAs
+                    STAMP(3);                              // prefetch issue
                     f32x4 dre, dim;
                     fir(pl, tbl, dre, dim);
+                    STAMP(4);                              // matched filter
                     emit_full<EM>(p, t * TS + wave * 256 - ld, dre, dim, kb);
+                    STAMP(5);                              // epilogue
                     __syncthreads();                       // LDS is restaged next trip
+                    STAMP(6);                              // end barrier
                 }
             } else {
                 __syncthreads();                           // `red` and the planes are reused
@@ -673,16 +703,19 @@ struct RxMfma {
                 emit_edge(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
                 __syncthreads();
                 ++t;
+                STAMP(7);                                  // general-path tiles
             }
         }
+        STAMP_FLUSH(blockIdx.x * (NT / 64) + wave);
     }
+
 };
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT>
 // (Capping this kernel at 4 waves/SIMD fits the steady loop in 128 registers but measured
-// slower on C3: 41.6 vs 35.7 us; left uncapped at 3.)
-__global__ __launch_bounds__(256) void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
+// slower on C3: 41.6 vs 35.7 us, with LDS still holding it at 3 workgroups per CU.)
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
+__global__ __launch_bounds__(NT) void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NT>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
     _Float16* pl = lds_h;                                   // 4 sample planes
     _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
@@ -776,19 +809,33 @@ static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s
                                      : rx_dec<InT, MIX_COMPLEX, OutT>(p, decim, s);
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT>
-static hipError_t rxm_go(const RxParams& p, const void* tables, hipStream_t s) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
+static hipError_t rxm_go_nt(const RxParams& p, const void* tables, hipStream_t s) {
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NT>;
     const int64_t ntiles = (p.nout + (p.k_first & 15) + K::TS - 1) / K::TS;
     const size_t lds = K::LDS_BYTES;
-    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT>);
-    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
+    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, NT>);
+    static const int cap = env_wgs_per_cu("MODEM_RX_WGS_PER_CU");
+    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, NT>), dim3(persistent_grid(k, K::NT, lds, ntiles, cap)),
                        dim3(K::NT), lds, s, p, static_cast<const _Float16*>(tables));
     return hipGetLastError();
 }
 
+template <int DEC, int NKS, typename InT, int MIX, typename OutT>
+static hipError_t rxm_go(const RxParams& p, const void* tables, hipStream_t s) {
+#ifdef MODEM_RX_NT64
+    return rxm_go_nt<DEC, NKS, InT, MIX, OutT, 64>(p, tables, s);
+#else
+    return rxm_go_nt<DEC, NKS, InT, MIX, OutT, 256>(p, tables, s);
+#endif
+}
+
 // (decim, k-steps) variants: W = 32 * nks >= 15 * decim + ntaps.
+#ifdef MODEM_DEV_MIN      // experiment builds: the C3 variant only
+#define RXM_TABLE(X) X(4, 6)
+#else
 #define RXM_TABLE(X) X(2, 2) X(2, 3) X(2, 5) X(2, 8) X(4, 3) X(4, 4) X(4, 6) X(4, 8) X(8, 5) X(8, 6) X(8, 9) X(8, 20)
+#endif
 
 template <typename InT, int MIX, typename OutT>
 static hipError_t rxm_sel(const RxParams& p, int decim, int nks, const void* tables, hipStream_t s) {
@@ -809,6 +856,10 @@ int rx_mfma_ksteps(int decim, int L) {
 
 hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const void* tables, int in_dtype,
                           int out_dtype, int mix, hipStream_t s) {
+#ifdef MODEM_DEV_MIN
+    if (in_dtype != 0 || out_dtype != 0 || mix != MIX_COMPLEX) return hipErrorInvalidValue;
+    return rxm_sel<float, MIX_COMPLEX, float>(p, decim, nks, tables, s);
+#endif
     auto go = [&](auto in_t, auto out_t) {
         using InT = decltype(in_t);
         using OutT = decltype(out_t);
@@ -821,6 +872,9 @@ hipError_t launch_rx_mfma(const RxParams& p, int decim, int nks, const void* tab
 
 hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, int mix,
                      hipStream_t s) {
+#ifdef MODEM_DEV_MIN
+    return hipErrorInvalidValue;
+#endif
     if (in_dtype == 1)
         return out_dtype == 1 ? rx_mixsel<__half, __half>(p, decim, mix, s)
                               : rx_mixsel<__half, float>(p, decim, mix, s);
@@ -830,3 +884,11 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
 
 
 }  // namespace mk
+
+#ifdef MODEM_STAMPS
+// Diagnostic builds only (tools/stamps.py): the per-wave segment cycle sums of the stamped
+// RX launches (same translation unit as the kernel that writes them).
+extern "C" int modem_debug_stamps(unsigned long long* host, size_t n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(mk::g_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
+}
+#endif

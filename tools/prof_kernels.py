@@ -25,6 +25,12 @@ def main():
             if a.only in ("rx", "both"):
                 r.rx(c)
     r.sync()
+    # coverage: poison the outputs, run the chain once more, then check every decision
+    for d in r.ch:
+        d["y"].fill_(float("nan"))
+        d["osym"].fill_(255)
+    r.step()
+    r.sync()
     print("ok", r.check())
 
 

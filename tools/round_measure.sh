@@ -9,7 +9,7 @@ out="$root/gpurun_out/$tag"
 mkdir -p "$out"
 cd "$root"
 echo "[1/4] gpu tests"
-timeout -k 10 420 python -m pytest tests -m gpu -q -x > "$out/gpu_tests.log" 2>&1 || { tail -30 "$out/gpu_tests.log"; exit 1; }
+timeout -k 10 420 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread > "$out/gpu_tests.log" 2>&1 || { tail -30 "$out/gpu_tests.log"; exit 1; }
 tail -1 "$out/gpu_tests.log"
 echo "[2/4] bench"
 timeout -k 10 300 python bench.py > "$out/bench.json" 2> "$out/bench.err" || { tail -20 "$out/bench.err"; exit 2; }
