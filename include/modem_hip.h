@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MODEM_HIP_ABI_VERSION 1
+#define MODEM_HIP_ABI_VERSION 2
 
 typedef enum {
     MODEM_OK = 0,
@@ -151,6 +151,13 @@ typedef struct {
     uint64_t s0;                 /* Carrier.sample at the first output sample */
     int32_t dtype;               /* modem_dtype of the output samples */
     int32_t out_mode;            /* modem_out_mode */
+    uint32_t q_offset;           /* 0: Bits source. samples_per_symbol / 2: EvenOddOffset(Bits)
+                                  * (data.rs:81-123, what modulate uses for oqpsk, modulate.rs:101-107):
+                                  * Q changes half a symbol after I, and before the first Q tick
+                                  * the phasor sees bit 0 (data.rs:84 `cur: [0, 0]`). Requires
+                                  * bits_per_symbol == 2 and an even samples_per_symbol
+                                  * (data.rs:91-92 asserts). With taps, the Q impulses sit at the
+                                  * Q ticks (GLUE). */
 } modem_tx_desc;
 
 modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out);

@@ -454,8 +454,24 @@ uint8_t or_slice(const or_slicer* s, float re, float im) {
 size_t or_tx_chain(or_phasor* p, const uint8_t* bits, size_t nbits, size_t sps,
                    const float* taps, size_t ntaps, float sf, uint64_t s0,
                    size_t flush_syms, int out_mode, float* out) {
+    return or_tx_chain_src(p, bits, nbits, sps, taps, ntaps, sf, s0, flush_syms, out_mode, 0, out);
+}
+
+size_t or_tx_chain_src(or_phasor* p, const uint8_t* bits, size_t nbits, size_t sps,
+                       const float* taps, size_t ntaps, float sf, uint64_t s0,
+                       size_t flush_syms, int out_mode, int even_odd, float* out) {
     or_carrier c; or_carrier_init(&c, sf, s0);
-    or_bits_source src; or_bits_init(&src, bits, nbits, sps, p->bits_per_symbol);
+    or_source inner; memset(&inner, 0, sizeof inner);
+    or_bits_init(&inner.bits, bits, nbits, sps, p->bits_per_symbol);
+    or_even_odd eo;
+    void* src = &inner;
+    int (*next)(void*, const uint8_t**) = or_source_next_v;
+    if (even_odd) {                                       /* modulate.rs:101-107 */
+        if (or_even_odd_init(&eo, &inner, sps, p->bits_per_symbol)) return 0;
+        src = &eo; next = or_even_odd_next_v;
+    }
+    const size_t half = sps / 2;
+    size_t n = 0;                                         /* samples of the data stream */
     or_fir fi, fq;
     if (ntaps) { or_fir_init(&fi, taps, ntaps); or_fir_init(&fq, taps, ntaps); }
     size_t k = 0, nflush = flush_syms * sps;
@@ -464,7 +480,7 @@ size_t or_tx_chain(or_phasor* p, const uint8_t* bits, size_t nbits, size_t sps,
         or_iq_sample s; int changed = 0;
         if (!finished) {
             or_carrier saved = c;
-            if (!or_dm_next(&c, p, or_bits_next_v, &src, &s, &changed)) {
+            if (!or_dm_next(&c, p, next, src, &s, &changed)) {
                 finished = 1; c = saved;      /* the Finished call's carrier tick is not a sample */
             }
         }
@@ -476,9 +492,14 @@ size_t or_tx_chain(or_phasor* p, const uint8_t* bits, size_t nbits, size_t sps,
         float xi = s.i, xq = s.q;
         if (ntaps) {                           /* GLUE: zero-stuff (impulse at the symbol tick) */
             if (!changed) { xi = 0.0f; xq = 0.0f; }
+            else if (even_odd && !finished) {  /* offset source: I ticks at n % sps == 0, Q ticks */
+                if (n % sps != 0) xi = 0.0f;   /* half a symbol later (data.rs:102-122)          */
+                if (n % sps != half) xq = 0.0f;
+            }
             xi = or_fir_add(&fi, xi);          /* fir.rs:27-34, one filter per rail */
             xq = or_fir_add(&fq, xq);
         }
+        if (!finished) n++;
         or_iq_sample y = { s.carrier, xi, xq };
         if (out_mode == OR_OUT_IQ_BASEBAND) { out[2 * k] = xi; out[2 * k + 1] = xq; }
         else {

@@ -167,6 +167,14 @@ size_t or_tx_chain(or_phasor* p, const uint8_t* bits, size_t nbits, size_t sps,
                    const float* taps, size_t ntaps, float sample_freq, uint64_t s0,
                    size_t flush_syms, int out_mode, float* out);
 
+/* The same with the source chosen as the modulate CLI does (modulate.rs:101-107): even_odd
+ * != 0 wraps the bits in EvenOddOffset (data.rs:81-123; bps == 2, sps even), so Q changes half
+ * a symbol after I. With taps, the I impulses sit at the I ticks (n % sps == 0) and the Q
+ * impulses at the Q ticks (n % sps == sps/2) — GLUE, parity unpinned by the reference. */
+size_t or_tx_chain_src(or_phasor* p, const uint8_t* bits, size_t nbits, size_t sps,
+                       const float* taps, size_t ntaps, float sample_freq, uint64_t s0,
+                       size_t flush_syms, int out_mode, int even_odd, float* out);
+
 /* RX chain, Demodulator loop structure: per input sample carrier.next() -> mix (complex
  * conjugate, or the reference's real-input mix with the 2x gain) -> FIRFilter on I and
  * Q at full rate -> keep n = k*sps + D -> slicer. Returns the number of symbols. */

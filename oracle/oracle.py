@@ -116,6 +116,7 @@ def lib():
         "or_prng_bits": (None, [u64, vp, sz]), "or_rrc_taps": (i, [sz, sz, c.c_double, fp]),
         "or_phasor_lut": (i, [P(Phasor), fp]), "or_slice": (u8, [P(Slicer), f, f]),
         "or_tx_chain": (sz, [P(Phasor), vp, sz, sz, fp, sz, f, u64, sz, i, fp]),
+        "or_tx_chain_src": (sz, [P(Phasor), vp, sz, sz, fp, sz, f, u64, sz, i, i, fp]),
         "or_rx_chain": (sz, [fp, sz, f, u64, i, fp, sz, sz, sz, P(Slicer), fp, vp, sz]),
         "or_modulate_cli": (c.c_long, [c.c_char_p, sz, sz, sz, sz, i, c.c_char_p, sz, fp, sz]),
     }
@@ -254,14 +255,16 @@ def qam_axis_slicer(bps: int, amplitude: float) -> Slicer:
 
 
 def tx_chain(p: Phasor, bits: np.ndarray, sps: int, taps: Optional[np.ndarray], sf: float, s0: int,
-             flush_syms: int = 0, out_mode: int = OUT_IQ_MIXED) -> np.ndarray:
+             flush_syms: int = 0, out_mode: int = OUT_IQ_MIXED, even_odd: bool = False) -> np.ndarray:
+    """or_tx_chain_src: DigitalModulator over Bits (or EvenOddOffset(Bits), data.rs:81-123)."""
     bits = np.ascontiguousarray(bits, np.uint8)
     nsym = len(bits) // p.bits_per_symbol + flush_syms
     per = 1 if out_mode == OUT_REAL else 2
     out = np.zeros(nsym * sps * per + 1, dtype=np.float32)
     t = np.zeros(1, np.float32) if taps is None else np.ascontiguousarray(taps, np.float32)
-    n = lib().or_tx_chain(ctypes.byref(p), bits.ctypes.data_as(ctypes.c_void_p), len(bits), sps, _fp(t),
-                          0 if taps is None else len(t), sf, s0, flush_syms, out_mode, _fp(out))
+    n = lib().or_tx_chain_src(ctypes.byref(p), bits.ctypes.data_as(ctypes.c_void_p), len(bits), sps, _fp(t),
+                              0 if taps is None else len(t), sf, s0, flush_syms, out_mode, int(even_odd),
+                              _fp(out))
     out = out[: n * per]
     return out if per == 1 else out.reshape(n, 2)
 

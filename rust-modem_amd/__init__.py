@@ -91,7 +91,8 @@ class _TxDesc(ctypes.Structure):
     _fields_ = [("bits_per_symbol", ctypes.c_uint32), ("lut", ctypes.POINTER(ctypes.c_float)),
                 ("samples_per_symbol", ctypes.c_uint32), ("taps", ctypes.POINTER(ctypes.c_float)),
                 ("ntaps", ctypes.c_uint32), ("sample_freq", ctypes.c_float),
-                ("s0", ctypes.c_uint64), ("dtype", ctypes.c_int32), ("out_mode", ctypes.c_int32)]
+                ("s0", ctypes.c_uint64), ("dtype", ctypes.c_int32), ("out_mode", ctypes.c_int32),
+                ("q_offset", ctypes.c_uint32)]
 
 
 class _RxDesc(ctypes.Structure):
@@ -420,11 +421,14 @@ class DigitalModulator:
     every complete symbol: (n, 2) interleaved (i, q) for the IQ modes, (n,) for OUT_REAL.
     `taps=None` keeps the reference's sample-and-hold (bit-compatible with `modulate --iq`).
     `carrier.sample` advances by the samples produced, as the shared `&mut Carrier` does.
+    `even_odd_offset=True` is the `EvenOddOffset` source (data.rs:81-123) that `modulate`
+    puts under OQPSK (modulate.rs:101-107): Q changes half a symbol after I; it panics
+    (ModemPanic) unless the phasor has 2 bits per symbol and samples_per_symbol is even.
     """
 
     def __init__(self, carrier: Carrier, phasor: _Phasor, samples_per_symbol: int,
                  taps: Optional[np.ndarray] = None, dtype: int = DTYPE_F32,
-                 out_mode: int = OUT_IQ_MIXED, device: int = 0):
+                 out_mode: int = OUT_IQ_MIXED, device: int = 0, even_odd_offset: bool = False):
         L = load_library()
         self.carrier, self.phasor = carrier, phasor
         self.sps, self.dtype, self.out_mode, self.device = int(samples_per_symbol), dtype, out_mode, device
@@ -440,6 +444,9 @@ class DigitalModulator:
         d.sample_freq = carrier.sample_freq
         d.s0 = carrier.sample
         d.dtype, d.out_mode = dtype, out_mode
+        d.q_offset = self._q_offset = self.sps // 2 if even_odd_offset else 0
+        if even_odd_offset and (self.bps != 2 or self.sps % 2):
+            raise ModemPanic(-1, "EvenOddOffset: bits_per_symbol == 2 and an even samples_per_symbol")
         h = ctypes.c_void_p()
         _check(L.modem_tx_create(ctypes.byref(d), device, ctypes.byref(h)), "DigitalModulator")
         self._h = h
@@ -469,7 +476,8 @@ class DigitalModulator:
 
     def flush(self, like=None, stream=None):
         ntaps = 0 if self.taps is None else len(self.taps)
-        ns = ((max(ntaps - 1, 0) + self.sps - 1) // self.sps) * self.sps
+        tail = ntaps - 1 + self._q_offset if ntaps else 0     # the delayed Q rail drains later
+        ns = ((tail + self.sps - 1) // self.sps) * self.sps
         ref = like if like is not None else np.zeros(1, np.uint8)
         out = self._alloc(ref, ns)
         prod = ctypes.c_size_t()

@@ -290,6 +290,8 @@ struct modem_tx {
     int dtype = 0, out_mode = 0;
     float2* d_lut = nullptr;
     float* d_taps = nullptr;
+    float* d_taps_q = nullptr;      // Q-rail taps when q_offset != 0
+    uint32_t q_offset = 0;
     float2* d_hist[2] = {nullptr, nullptr};
     uint8_t* d_carry[2] = {nullptr, nullptr};
     int hcur = 0, ccur = 0, ncarry = 0;
@@ -303,7 +305,7 @@ struct modem_tx {
     Stage bits_stage, out_stage;
     ~modem_tx() {
         DeviceGuard g(device);
-        for (void* p : {(void*)d_lut, (void*)d_taps, (void*)d_hist[0], (void*)d_hist[1],
+        for (void* p : {(void*)d_lut, (void*)d_taps, (void*)d_taps_q, (void*)d_hist[0], (void*)d_hist[1],
                         (void*)d_carry[0], (void*)d_carry[1], (void*)d_bfrag, (void*)d_luth})
             if (p) (void)hipFree(p);
     }
@@ -322,6 +324,10 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     if (d->ntaps > (uint32_t)mk::kMaxTaps || (d->ntaps && !d->taps)) return MODEM_ERR_INVALID_ARG;
     if (d->dtype != MODEM_DTYPE_F32 && d->dtype != MODEM_DTYPE_F16) return MODEM_ERR_INVALID_ARG;
     if (d->out_mode < MODEM_OUT_IQ_MIXED || d->out_mode > MODEM_OUT_REAL) return MODEM_ERR_INVALID_ARG;
+    // EvenOddOffset::new asserts bits_per_symbol == 2 and an even samples_per_symbol (data.rs:91-92)
+    if (d->q_offset != 0 && (d->bits_per_symbol != 2 || d->samples_per_symbol % 2 != 0 ||
+                             d->q_offset != d->samples_per_symbol / 2))
+        return MODEM_ERR_INVALID_ARG;
     if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
     DeviceGuard g(device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
@@ -335,23 +341,42 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     h->sample = d->s0;
     h->dtype = d->dtype;
     h->out_mode = d->out_mode;
-    // ntaps == 0: the reference's sample-and-hold == zero-stuffing + sps unit taps.
+    h->q_offset = d->q_offset;
+    // ntaps == 0: the reference's sample-and-hold == zero-stuffing + sps unit taps. A Q offset
+    // D delays the Q rail: its taps are h[j - D] (length L + D).
     const uint32_t L = d->ntaps ? d->ntaps : d->samples_per_symbol;
-    h->K = (L + h->sps - 1) / h->sps;
+    const uint32_t D = d->q_offset;
+    h->K = (L + D + h->sps - 1) / h->sps;
     // pp[t*sps + p] = h[p + sps*t]; padded by mk::kTapPad steps of zeros so the kernels'
     // look-ahead tap loads stay in bounds.
-    std::vector<float> pp((size_t)(h->K + mk::kTapPad) * h->sps, 0.0f);
-    for (uint32_t j = 0; j < L; ++j) pp[(size_t)(j / h->sps) * h->sps + j % h->sps] = d->ntaps ? d->taps[j] : 1.0f;
+    std::vector<float> pp((size_t)(h->K + mk::kTapPad) * h->sps, 0.0f), pq;
+    auto tap = [&](uint32_t j) { return d->ntaps ? d->taps[j] : 1.0f; };
+    for (uint32_t j = 0; j < L; ++j) pp[(size_t)(j / h->sps) * h->sps + j % h->sps] = tap(j);
+    if (D) {
+        pq.assign(pp.size(), 0.0f);
+        for (uint32_t j = 0; j < L; ++j) pq[(size_t)((j + D) / h->sps) * h->sps + (j + D) % h->sps] = tap(j);
+    }
     modem_status st;
     const size_t nl = (size_t)1 << h->bps;
     if ((st = dalloc(&h->d_lut, nl)) || (st = dalloc(&h->d_taps, pp.size())) ||
         (st = dalloc(&h->d_hist[0], h->K)) || (st = dalloc(&h->d_hist[1], h->K)) ||
-        (st = dalloc(&h->d_carry[0], 8)) || (st = dalloc(&h->d_carry[1], 8))) {
+        (st = dalloc(&h->d_carry[0], 8)) || (st = dalloc(&h->d_carry[1], 8)) ||
+        (D && (st = dalloc(&h->d_taps_q, pq.size())))) {
         delete h;
         return st;
     }
     if (hipMemcpy(h->d_lut, d->lut, nl * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->d_taps, pp.data(), pp.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(h->d_taps, pp.data(), pp.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        (D && hipMemcpy(h->d_taps_q, pq.data(), pq.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)) {
+        (void)hipGetLastError();
+        delete h;
+        return MODEM_ERR_HIP;
+    }
+    // Sample-and-hold EvenOddOffset: before the first Q tick the phasor sees cur = [b0, 0]
+    // (data.rs:84), i.e. the Q value of symbol index 0; it enters as the history symbol that
+    // the delayed Q rail reads for n < D (its I value meets zero taps).
+    if (D && d->ntaps == 0 &&
+        hipMemcpy(h->d_hist[0] + (h->K - 2), d->lut, sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipGetLastError();
         delete h;
         return MODEM_ERR_HIP;
@@ -361,7 +386,7 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     const char* env = std::getenv("MODEM_HIP_FIR");
     const bool force_valu = env && std::strcmp(env, "valu") == 0;
     // Sample-and-hold (no taps) stays on the VALU kernels, which reproduce it bit for bit.
-    h->mfma_ksteps = (force_valu || d->ntaps == 0) ? 0 : mk::tx_mfma_ksteps((int)h->sps, (int)h->K);
+    h->mfma_ksteps = (force_valu || d->ntaps == 0 || D) ? 0 : mk::tx_mfma_ksteps((int)h->sps, (int)h->K);
     if (h->mfma_ksteps > 0) {
         // Split-f16 operands of tx_mfma (modem_tx.hip). Exact power-of-two scales put the
         // maxima of the LUT and of the taps in [2^14, 2^15); both are split hi + lo =
@@ -437,7 +462,7 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     if (!h || !produced || (nbits && !bits)) return MODEM_ERR_INVALID_ARG;
     *produced = 0;
     const uint64_t total = (uint64_t)h->ncarry + nbits;
-    const int64_t nsym = flush ? (int64_t)((h->ntaps ? h->ntaps - 1 : 0) + h->sps - 1) / h->sps
+    const int64_t nsym = flush ? (int64_t)((h->ntaps ? h->ntaps - 1 + h->q_offset : 0) + h->sps - 1) / h->sps
                                : (int64_t)(total / h->bps);
     const int ncarry_new = flush ? h->ncarry : (int)(total - (uint64_t)nsym * h->bps);
     const size_t nsamp = (size_t)nsym * h->sps;
@@ -466,6 +491,7 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     p.hist_new = h->d_hist[h->hcur ^ 1];
     p.lut = h->d_lut;
     p.taps = h->d_taps;
+    p.taps_q = h->d_taps_q;
     p.out = dout;
     p.s0 = h->sample;
     p.nsym = nsym;

@@ -16,6 +16,7 @@ struct TxParams {
     float2* hist_new;        // K-1 values preceding the next call's symbol 0
     const float2* lut;       // 2^bps complex points (device)
     const float* taps;       // polyphase taps, taps[t*sps + p] = h[p + sps*t], K*sps floats
+    const float* taps_q;     // Q-rail taps (the I taps delayed by the Q offset), or null: = taps
     void* out;               // f32 or f16 samples (layout per out_mode)
     uint64_t s0;             // carrier sample of output sample 0
     int64_t nsym;            // symbols this call emits

@@ -585,11 +585,11 @@ __global__ __launch_bounds__(256) void tx_generic(const TxParams p) {
     for (int i = threadIdx.x; i < nsamp; i += NT) {
         const int ml = i / SPS, q = i - ml * SPS;
         float yr = 0.f, yi = 0.f;
+        const float* tq = p.taps_q ? p.taps_q : p.taps;   // EvenOddOffset: Q rail delayed
         for (int t = 0; t < K; ++t) {
-            const float h = p.taps[t * SPS + q];
             const float2 a = lds[ml - t + K - 1];
-            yr = __builtin_fmaf(a.x, h, yr);
-            yi = __builtin_fmaf(a.y, h, yi);
+            yr = __builtin_fmaf(a.x, p.taps[t * SPS + q], yr);
+            yi = __builtin_fmaf(a.y, tq[t * SPS + q], yi);
         }
         tx_emit<OUT_MODE, OutT>(p, m0 * SPS + i, make_float2(yr, yi), make_float2(0.f, 0.f), false);
     }
@@ -609,7 +609,7 @@ static hipError_t tx_go(const TxParams& p, hipStream_t s) {
 
 template <int OM, typename OutT>
 static hipError_t tx_sps(const TxParams& p, int sps, hipStream_t s) {
-    switch (sps) {
+    switch (p.taps_q ? 0 : sps) {                  // a delayed Q rail: generic kernel
     case 1: return tx_go<1, OM, OutT>(p, s);
     case 2: return tx_go<2, OM, OutT>(p, s);
     case 4: return tx_go<4, OM, OutT>(p, s);
