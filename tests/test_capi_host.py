@@ -194,3 +194,22 @@ def test_product_luts_match_fixtures(m):
         for key, ph in (("bpsk_pi4", m.BPSK(PI_4, 1.0)), ("qpsk", m.QPSK(0.0, 1.0)),
                         ("qam16", m.QAM(4, 0.0, 1.0)), ("qam256", m.QAM(8, 0.0, 1.0))):
             assert np.array_equal(ph.lut().view(np.uint32), z[key].view(np.uint32)), key
+
+
+# ------------------------------------------------------------ modulate CLI (host side) ----
+def _cli(args, stdin=b"0101"):
+    import subprocess
+    exe = os.path.join(ROOT, "rust-modem_amd", "bin", "modulate")
+    return subprocess.run([exe] + args, input=stdin, capture_output=True, timeout=60).returncode
+
+
+def test_modulate_cli_argument_panics():
+    """modulate.rs panics (exit 101) before any device work; stateful phasors exit 2."""
+    assert _cli([]) == 101                                  # -m is required (modulate.rs:42)
+    assert _cli(["-m", "nope"]) == 101                      # modulate.rs:94
+    assert _cli(["-m", "qpsk", "-r", "x"]) == 101           # invalid sample rate
+    assert _cli(["-m", "qpsk", "-c", "6000"]) == 101        # cf < sr / 2 (modulate.rs:68)
+    assert _cli(["-m", "qpsk", "-c", "900", "-p", "1"]) == 101   # sr % cf == 0 (modulate.rs:62)
+    for s in ("bfsk", "msk", "mfsk", "16cpfsk", "dcqpsk", "dqpsk", "dbpsk"):
+        assert _cli(["-m", s]) == 2
+    assert _cli(["-h"]) == 0

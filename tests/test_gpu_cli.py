@@ -1,0 +1,84 @@
+"""The `modulate` drop-in (rust-modem_amd/bin/modulate) against the
+oracle's restatement of src/bin/modulate.rs (or_modulate_cli) on the same stdin.
+
+--iq output: bit-exact. Passband output (real part, with and without the preamble): within the
+f32 sample tolerance (hardware sin/cos vs glibc). Panics of the reference exit with 101 after
+the samples of the symbols before the bad digit; stateful phasors exit with 2.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "rust-modem_amd", "bin", "modulate")
+MODS = ["bask", "bpsk", "qpsk", "qam16", "qam256", "16psk", "oqpsk", "16apsk"]
+
+pytestmark = pytest.mark.gpu
+
+
+def bits_text(o, seed, nbits):
+    bits = o.prng_bits(seed, nbits)
+    s = "".join("1" if b else "0" for b in bits)
+    # whitespace anywhere is skipped (data.rs:150-152), including U+0085 / U+00A0 bytes
+    return (s[:7] + " \n" + s[7:40] + "\t" + s[40:]).encode() + b"\x85\xa0\n"
+
+
+def run_cli(args, stdin):
+    env = dict(os.environ)
+    r = subprocess.run([CLI] + args, input=stdin, capture_output=True, env=env, timeout=60)
+    return r.returncode, np.frombuffer(r.stdout, dtype="<f4"), r.stderr
+
+
+def oracle_cli(o, mod, sr, br, cf, pc, iq, text):
+    cap = 4 * len(text) * (sr // br + 1) + sr // max(cf, 1) * (pc + 1) + 64
+    out = np.zeros(cap, np.float32)
+    t = text.replace(b"\x85", b" ").replace(b"\xa0", b" ")    # the oracle's reader skips ASCII only
+    k = o.lib().or_modulate_cli(mod.encode(), sr, br, cf, pc, int(iq), t, len(t),
+                                out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), cap)
+    assert k >= 0, f"oracle panicked for {mod}"
+    return out[:k]
+
+
+@pytest.mark.parametrize("mod", MODS)
+def test_cli_iq_bit_exact(o, torch_cuda, mod):
+    text = bits_text(o, 11, 8 * 300 + 3)
+    rc, got, err = run_cli(["-m", mod, "-r", "10000", "-b", "1250", "--iq"], text)
+    assert rc == 0, err
+    ref = oracle_cli(o, mod, 10000, 1250, 1000, 0, True, text)
+    assert got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("mod", ["qpsk", "qam16", "oqpsk", "16apsk"])
+@pytest.mark.parametrize("pc", [0, 3])
+def test_cli_passband(o, torch_cuda, mod, pc):
+    text = bits_text(o, 12, 8 * 200)
+    # defaults: -r 10000 -b 220 -c 1000 (45 samples per symbol); EvenOddOffset needs an even
+    # count (data.rs:92), so oqpsk runs at 250 baud
+    br = 250 if mod == "oqpsk" else 220
+    args = ["-m", mod] + (["-b", str(br)] if br != 220 else []) + (["-p", str(pc)] if pc else [])
+    rc, got, err = run_cli(args, text)
+    assert rc == 0, err
+    ref = oracle_cli(o, mod, 10000, br, 1000, pc, False, text)
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= 1e-5 * max(np.abs(ref).max(), 1.0)
+
+
+def test_cli_bad_digit_panics_after_complete_symbols(o, torch_cuda):
+    good = bits_text(o, 13, 4 * 50)
+    rc, got, _ = run_cli(["-m", "qam16", "-b", "2500", "--iq"], good + b"10" + b"2" + b"0101")
+    assert rc == 101
+    ref = oracle_cli(o, "qam16", 10000, 2500, 1000, 0, True, good)   # the 2 leftover bits never form a symbol
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+def test_cli_stateful_and_invalid(torch_cuda):
+    assert run_cli(["-m", "bfsk"], b"0101")[0] == 2
+    assert run_cli(["-m", "nope"], b"0101")[0] == 101
+    assert run_cli([], b"0101")[0] == 101                            # -m is required
+    assert run_cli(["-m", "qpsk", "-c", "6000"], b"0101")[0] == 101   # cf < sr / 2 (modulate.rs:68)
+    assert run_cli(["-m", "qpsk", "-c", "900", "-p", "2"], b"0101")[0] == 101   # sr % cf (modulate.rs:62)
+    assert run_cli(["-m", "oqpsk"], b"0101")[0] == 101               # 45 samples/symbol: data.rs:92
