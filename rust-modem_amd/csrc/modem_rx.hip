@@ -420,13 +420,33 @@ struct RxMfma {
     static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
     static constexpr int NQ = (NS + 3) / 4;                     // quads
     static constexpr int U = (NQ + NT - 1) / NT;                // quads per lane
-    static constexpr int PL = (rxh_pos(4 * NQ - 1, RW) + 1 + 7) & ~7;   // halves per plane
+    // Plane layout. decim 4 (4 waves): unpadded, 16-B chunks XOR-swizzled within each aligned
+    // group of 8 chunks — conflict-free A reads (tests/test_lds_banks.py) and 4 KiB less LDS
+    // per workgroup than padding, which lets 4 workgroups share a CU. Otherwise rxh_pos.
+#ifdef MODEM_RX_NOSWZ
+    static constexpr bool SWZ = false;
+#else
+    static constexpr bool SWZ = DEC == 4 && NT == 256;
+#endif
+    __host__ __device__ static constexpr int ppos(int e) {    // plane position of staged sample e
+        return SWZ ? ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7)) : rxh_pos(e, RW);
+    }
+    static constexpr int PL = SWZ ? (4 * NQ + 63) & ~63 : (rxh_pos(4 * NQ - 1, RW) + 1 + 7) & ~7;   // halves per plane
     static constexpr int NC = rx_mfma_table_copies(DEC);
     static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
     static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 16;   // + red
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
+    // Waves per SIMD the registers are held to: 4 for the swizzled layout (its LDS lets 4
+    // workgroups share a CU; the matched filter then single-buffers its operands to fit 128
+    // VGPRs: 35.0 vs 35.4 us on C3), else the compiler's choice (3 on C3).
+#ifdef MODEM_RX_NOWPE
+    static constexpr int WPE = 1;
+#else
+    static constexpr int WPE = SWZ && LDS_BYTES <= 40960 ? 4 : 1;
+#endif
     static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
-    static constexpr int SLOT_POS = 4 * NT + 16 * (4 * NT / RW);  // plane offset between slots
+    // plane offset between staging slots (the swizzle repeats every 1024 samples)
+    static constexpr int SLOT_POS = SWZ ? 4 * NT : 4 * NT + 16 * (4 * NT / RW);
 
     // Rows hold 16 instants aligned to the absolute instant index (k % 16 == column), so an
     // instant's taps always fall at the same k positions of the 32-wide MFMA sums and the
@@ -479,7 +499,7 @@ struct RxMfma {
         // carrier index of the lane's first sample; opaque, so that the per-sample offsets
         // stay immediates instead of 4*U hoisted loop-invariant VGPRs
         uint32_t lb = nb32 + 4u * (uint32_t)tid;
-        int pos0 = rxh_pos(4 * tid, RW);                  // slot u writes at pos0 + u * SLOT_POS
+        int pos0 = ppos(4 * tid);                         // slot u writes at pos0 + u * SLOT_POS
         asm volatile("" : "+v"(lb), "+v"(pos0));
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         float mx = 0.f;
@@ -543,7 +563,7 @@ struct RxMfma {
                                              : make_float2(0.f, 0.f);
                 zr[j] = z.x; zi[j] = z.y;
             }
-            put4o(pl, rxh_pos(e0, RW), zr, zi, sc);
+            put4o(pl, ppos(e0), zr, zi, sc);
         }
         return ka;
     }
@@ -554,6 +574,7 @@ struct RxMfma {
         const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
         const int i = lane & 15, g = lane >> 4;
         const _Float16* arow = pl + (16 * wave + i) * RP + 8 * g;
+        const int ae = (16 * wave + i) * RW + 8 * g;            // sample of this lane's first A read
         const int xb = 8 * g + (15 - i) * DEC;                  // B start for this lane's column
         const int q = xb & 7;                                   // copy with Tq[y] = T[y + q]
         const _Float16* brow = tbl + (q / (8 / NC)) * 2 * TB + (xb - q);
@@ -567,19 +588,22 @@ struct RxMfma {
         auto aoff = [](int s) { return 32 * s + 16 * ((32 * s) / RW); };
         h8 a[2][4], b[2][2];
         auto load = [&](int s, int slot) {
-            const int o = aoff(s);
-            a[slot][0] = *reinterpret_cast<const h8*>(arow + o);
-            a[slot][1] = *reinterpret_cast<const h8*>(arow + PL + o);
-            a[slot][2] = *reinterpret_cast<const h8*>(arow + 2 * PL + o);
-            a[slot][3] = *reinterpret_cast<const h8*>(arow + 3 * PL + o);
+            const _Float16* ap = SWZ ? pl + ppos(ae + 32 * s) : arow + aoff(s);
+            a[slot][0] = *reinterpret_cast<const h8*>(ap);
+            a[slot][1] = *reinterpret_cast<const h8*>(ap + PL);
+            a[slot][2] = *reinterpret_cast<const h8*>(ap + 2 * PL);
+            a[slot][3] = *reinterpret_cast<const h8*>(ap + 3 * PL);
             b[slot][0] = *reinterpret_cast<const h8*>(brow + 32 * s);
             b[slot][1] = *reinterpret_cast<const h8*>(brow + TB + 32 * s);
         };
-        load(0, 0);
+        // WPE 4: single-buffered operands (fewer registers; the other waves hide the LDS
+        // latency); otherwise the next k-step's operands load during this one's products
+        if (WPE < 4) load(0, 0);
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
-            const int c = s & 1;
-            if (s + 1 < NKS) load(s + 1, c ^ 1);
+            const int c = WPE < 4 ? s & 1 : 0;
+            if (WPE >= 4) load(s, 0);
+            else if (s + 1 < NKS) load(s + 1, c ^ 1);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][0], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
@@ -714,7 +738,8 @@ struct RxMfma {
 // (Capping this kernel at 4 waves/SIMD fits the steady loop in 128 registers but measured
 // slower on C3: 41.6 vs 35.7 us, with LDS still holding it at 3 workgroups per CU.)
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
-__global__ __launch_bounds__(NT) void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NT>::WPE)))
+void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
     using K = RxMfma<DEC, NKS, InT, MIX, OutT, NT>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
     _Float16* pl = lds_h;                                   // 4 sample planes

@@ -86,3 +86,27 @@ def test_old_layout_matches_measured_conflicts():
     assert a_cost(4, 6, 8) == 4
     assert b_cost(4, 6, old_residue) == 4
     assert 24 * a_cost(4, 6, 8) + 12 * b_cost(4, 6, old_residue) == 144
+
+
+def swz_pos(e):
+    """RxMfma::ppos for decim 4 (4 waves): 16-B chunks XOR-swizzled within groups of 8."""
+    return ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7))
+
+
+def test_swizzled_layout_conflict_free():
+    # A reads: lane (i, g) of wave w, k-step s reads 8 halves at sample (16 w + i) * 64 + 8 g + 32 s
+    for w in range(4):
+        for s in range(8):
+            assert extra_cycles(lambda l: 2 * swz_pos((16 * w + (l & 15)) * 64 + 8 * (l >> 4) + 32 * s)) == 0
+    # staging writes: ds_write_b64, 4 groups of 16 contiguous lanes, bank = (a / 4) mod 32
+    for u in range(5):
+        for g in range(4):
+            banks = {}
+            for lane in range(16 * g, 16 * g + 16):
+                a = 2 * (swz_pos(4 * lane) + 1024 * u)
+                for d in range(2):
+                    banks.setdefault((a // 4 + d) % 32, set()).add(a)
+            assert max(len(v) for v in banks.values()) == 1
+    # a bijection within every aligned group of 8 chunks (no LDS beyond the unpadded plane)
+    for base in range(0, 4096, 64):
+        assert sorted(swz_pos(e) for e in range(base, base + 64)) == list(range(base, base + 64))
