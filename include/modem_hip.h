@@ -89,7 +89,14 @@ typedef enum {
     MODEM_PHASOR_BASK = 4,   /* BASK::new(amplitude)                   bask.rs:8-12 */
     MODEM_PHASOR_MPSK = 5,   /* MPSK::new(bps, phase_offset, amp)      mpsk.rs:14-21 */
     MODEM_PHASOR_APSK = 6,   /* APSK::new(amplitude, bps, rings)       apsk.rs:25-33 */
-    MODEM_PHASOR_OQPSK = 7   /* OQPSK::new(amplitude) (symbol map only) oqpsk.rs:9-13 */
+    MODEM_PHASOR_OQPSK = 7,  /* OQPSK::new(amplitude) (symbol map only) oqpsk.rs:9-13 */
+    /* Phasors whose (i, q) also depend on the symbol count or the sample index. They have no
+     * LUT (modem_phasor_lut returns MODEM_ERR_UNSUPPORTED): pass the descriptor to
+     * modem_tx_create as modem_tx_desc.phasor (sample-and-hold only, ntaps == 0). */
+    MODEM_PHASOR_DCQPSK = 8, /* DCQPSK::new(amplitude)                 dcqpsk.rs:16-21 */
+    MODEM_PHASOR_CPFSK = 10, /* CPFSK::new(bps, rates, amp, deviation) cpfsk.rs:15-25; freq =
+                              * Freq::new(deviation * baud / 2, sr).sample_freq() */
+    MODEM_PHASOR_MSK = 11    /* MSK::new(amplitude, samples_per_symbol) msk.rs:13-21 */
 } modem_phasor_kind;
 
 typedef struct { uint8_t start, end; float radius, phase; } modem_ring; /* apsk.rs:60-82 */
@@ -101,6 +108,8 @@ typedef struct {
     float amplitude;
     uint32_t nrings;             /* APSK */
     const modem_ring* rings;     /* APSK */
+    float freq;                  /* CPFSK: its sample frequency (cpfsk.rs:20-21) */
+    uint32_t samples_per_symbol; /* MSK: samples per symbol (even, msk.rs:14) */
 } modem_phasor_desc;
 
 /* Slicer description; fill it with modem_phasor_slicer() or by hand. */
@@ -143,7 +152,8 @@ modem_status modem_rrc_taps(uint32_t ntaps, uint32_t sps, double beta, float* ou
 typedef struct modem_tx modem_tx;
 typedef struct {
     uint32_t bits_per_symbol;    /* 1..8 */
-    const float* lut;            /* 2 * 2^bps floats from modem_phasor_lut (host memory) */
+    const float* lut;            /* 2 * 2^bps floats from modem_phasor_lut (host memory);
+                                  * unused when `phasor` is set */
     uint32_t samples_per_symbol; /* Rates::samples_per_symbol, >= 1 */
     const float* taps;           /* pulse-shaping FIR (host memory) */
     uint32_t ntaps;              /* 0 = the reference's sample-and-hold (no FIR) */
@@ -158,6 +168,10 @@ typedef struct {
                                   * bits_per_symbol == 2 and an even samples_per_symbol
                                   * (data.rs:91-92 asserts). With taps, the Q impulses sit at the
                                   * Q ticks (GLUE). */
+    const modem_phasor_desc* phasor; /* NULL, or a DCQPSK / CPFSK / MSK phasor evaluated per
+                                  * sample as DigitalModulator does (modulator.rs:85-100: the
+                                  * symbol count since the stream start, and the carrier sample
+                                  * index after Carrier::next); copied at create. */
 } modem_tx_desc;
 
 modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out);

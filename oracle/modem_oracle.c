@@ -212,6 +212,27 @@ int or_dmpsk_new(or_phasor* p, size_t bps, float amplitude, float phase, float s
     p->bits_per_symbol = bps; p->amplitude = amplitude; p->phase = phase; p->shift = shift;
     return 0;
 }
+int or_cpfsk_new(or_phasor* p, size_t bps, size_t br, size_t sr, float amplitude, size_t deviation) {
+    if (sr == 0) return -1;                               /* Freq::new divides by sr */
+    or_phasor_zero(p, OR_CPFSK);                          /* cpfsk.rs:15-25 */
+    p->bits_per_symbol = bps; p->amplitude = amplitude;
+    p->freq = or_freq_sample_freq(deviation * br / 2, sr);   /* Freq::new(dev*br/2, sr), :20-21 */
+    return 0;
+}
+int or_msk_new(or_phasor* p, float amplitude, size_t sps) {                  /* msk.rs:13-21 */
+    if (sps % 2 != 0) return -1;                          /* msk.rs:14 */
+    or_phasor_zero(p, OR_MSK);
+    p->amplitude = amplitude; p->samples_per_bit = sps / 2; p->bits_per_symbol = 2;
+    return 0;
+}
+static float or_cpfsk_inner(const or_phasor* p, const uint8_t* b, size_t n, uint64_t s) {
+    float coef = 2.0f * (float)or_bytes_to_bits(b, n);   /* cpfsk.rs:27-29 */
+    return coef * p->freq * (float)s;                     /* cpfsk.rs:31-33, left to right */
+}
+static float or_msk_inner(const or_phasor* p, uint64_t s) {                  /* msk.rs:23-25 */
+    return OR_PI / 2.0f * (float)s / (float)p->samples_per_bit;
+}
+
 size_t or_phasor_bits_per_symbol(const or_phasor* p) { return p->bits_per_symbol; }
 
 static float or_qam_pos(const or_phasor* p, const uint8_t* b, size_t n) {   /* qam.rs:32-38 */
@@ -239,8 +260,9 @@ void or_phasor_update(or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
 }
 
 float or_phasor_i(const or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
-    (void)s;
     switch (p->kind) {
+    case OR_CPFSK: return p->amplitude * cosf(or_cpfsk_inner(p, b, n, s));   /* cpfsk.rs:39-41 */
+    case OR_MSK: return p->amplitude * or_bit_to_sign(b[0]) * cosf(or_msk_inner(p, s)); /* msk.rs:31-33 */
     case OR_BPSK: return (or_bit_to_sign(b[0]) * p->amplitude) * cosf(p->phase); /* bpsk.rs:17-27 */
     case OR_QPSK: return p->amplitude * (or_bit_to_sign(b[0]) * p->phase_cos -
                                          or_bit_to_sign(b[1]) * p->phase_sin); /* qpsk.rs:23-28 */
@@ -263,8 +285,9 @@ float or_phasor_i(const or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
     return 0.0f;
 }
 float or_phasor_q(const or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
-    (void)s;
     switch (p->kind) {
+    case OR_CPFSK: return p->amplitude * sinf(or_cpfsk_inner(p, b, n, s));   /* cpfsk.rs:43-45 */
+    case OR_MSK: return -p->amplitude * or_bit_to_sign(b[1]) * sinf(or_msk_inner(p, s)); /* msk.rs:35-37 */
     case OR_BPSK: return (or_bit_to_sign(b[0]) * p->amplitude) * sinf(p->phase); /* bpsk.rs:29-31 */
     case OR_QPSK: return p->amplitude * (or_bit_to_sign(b[1]) * p->phase_cos +
                                          or_bit_to_sign(b[0]) * p->phase_sin); /* qpsk.rs:30-35 */
@@ -565,13 +588,15 @@ long or_modulate_cli(const char* name, size_t sr, size_t br, size_t cf, size_t p
     }
     else if (!strcmp(name, "dqpsk")) or_dmpsk_new(&p, 2, AMPLITUDE, OR_PI / 4.0f, OR_PI / 2.0f);
     else if (!strcmp(name, "dbpsk")) or_dmpsk_new(&p, 1, AMPLITUDE, OR_PI / 4.0f, OR_PI);
-    else return -2;                                       /* bfsk/msk/mfsk/16cpfsk: out of scope */
+    else if (!strcmp(name, "msk")) { if (or_msk_new(&p, AMPLITUDE, sps)) return -1; }    /* :81 */
+    else if (!strcmp(name, "16cpfsk")) or_cpfsk_new(&p, 4, br, sr, AMPLITUDE, 1);       /* :87 */
+    else return -2;                                       /* bfsk/mfsk: out of scope */
 
     or_source bits; memset(&bits, 0, sizeof bits);        /* :98-99 */
     bits.is_ascii = 1; or_ascii_init(&bits.ascii, text, len, sps, p.bits_per_symbol);
     or_even_odd eo;
     void* src = &bits; int (*next)(void*, const uint8_t**) = or_source_next_v;
-    if (!strcmp(name, "oqpsk")) {                         /* :101-107 */
+    if (!strcmp(name, "oqpsk") || !strcmp(name, "msk")) { /* :101-107 */
         if (or_even_odd_init(&eo, &bits, sps, p.bits_per_symbol)) return -1;
         src = &eo; next = or_even_odd_next_v;
     }

@@ -78,7 +78,8 @@ class _Ring(ctypes.Structure):
 class _PhasorDesc(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("bits_per_symbol", ctypes.c_uint32),
                 ("phase", ctypes.c_float), ("amplitude", ctypes.c_float),
-                ("nrings", ctypes.c_uint32), ("rings", ctypes.POINTER(_Ring))]
+                ("nrings", ctypes.c_uint32), ("rings", ctypes.POINTER(_Ring)),
+                ("freq", ctypes.c_float), ("samples_per_symbol", ctypes.c_uint32)]
 
 
 class _SlicerDesc(ctypes.Structure):
@@ -92,7 +93,7 @@ class _TxDesc(ctypes.Structure):
                 ("samples_per_symbol", ctypes.c_uint32), ("taps", ctypes.POINTER(ctypes.c_float)),
                 ("ntaps", ctypes.c_uint32), ("sample_freq", ctypes.c_float),
                 ("s0", ctypes.c_uint64), ("dtype", ctypes.c_int32), ("out_mode", ctypes.c_int32),
-                ("q_offset", ctypes.c_uint32)]
+                ("q_offset", ctypes.c_uint32), ("phasor", ctypes.POINTER(_PhasorDesc))]
 
 
 class _RxDesc(ctypes.Structure):
@@ -325,7 +326,8 @@ class MPSK(_Phasor):
 
 
 class OQPSK(_Phasor):
-    """oqpsk.rs:4-26 (the symbol map; the half-symbol Q offset source is not on the GPU path)."""
+    """oqpsk.rs:4-26 (the symbol map; pair it with DigitalModulator(even_odd_offset=True),
+    the EvenOddOffset source modulate uses, modulate.rs:101-107)."""
     _kind = _PH_OQPSK
 
     def __init__(self, amplitude: float):
@@ -358,6 +360,61 @@ class APSK(_Phasor):
         self._rings_c = arr
         d.nrings = len(self.rings)
         d.rings = ctypes.cast(arr, ctypes.POINTER(_Ring))
+        return d
+
+
+class _SamplePhasor(_Phasor):
+    """A DigitalPhasor whose (i, q) also depend on the symbol count or the sample index: no
+    bits-only table; DigitalModulator evaluates it per sample on the GPU (tx_phasor)."""
+    sample_dependent = True
+
+    def lut(self) -> np.ndarray:
+        raise ModemError(ERR_UNSUPPORTED, f"{type(self).__name__} has no bits-only (I,Q) table")
+
+    def slicer(self):
+        raise ModemError(ERR_UNSUPPORTED, f"{type(self).__name__}: no memoryless slicer")
+
+    def i(self, s, b):
+        raise ModemError(ERR_UNSUPPORTED, "evaluated per sample inside DigitalModulator")
+
+    q = i
+
+
+class DCQPSK(_SamplePhasor):
+    """dcqpsk.rs:8-53 (pi/4-QPSK: the constellation turns by pi/4 at every symbol)."""
+    _kind = 8
+
+    def __init__(self, amplitude: float):
+        self.amplitude = float(amplitude)
+
+
+class CPFSK(_SamplePhasor):
+    """cpfsk.rs:9-45: CPFSK::new(bits_per_symbol, rates, amplitude, deviation)."""
+    _kind = 10
+
+    def __init__(self, bits_per_symbol: int, rates: "Rates", amplitude: float, deviation: int):
+        self._bps, self.amplitude = int(bits_per_symbol), float(amplitude)
+        self._freq = Freq(int(deviation) * rates.baud_rate // 2, rates.sample_rate).sample_freq()
+
+    def _desc(self):
+        d = super()._desc()
+        d.freq = self._freq
+        return d
+
+
+class MSK(_SamplePhasor):
+    """msk.rs:6-37: MSK::new(amplitude, samples_per_symbol) (modulate pairs it with the
+    EvenOddOffset source, modulate.rs:101-107: DigitalModulator(even_odd_offset=True))."""
+    _kind = 11
+
+    def __init__(self, amplitude: float, samples_per_symbol: int):
+        if int(samples_per_symbol) % 2 != 0:
+            raise ModemPanic(ERR_INVALID_ARG, "MSK::new: assertion failed: samples_per_symbol % 2 == 0")
+        self.amplitude, self._sps = float(amplitude), int(samples_per_symbol)
+
+    def _desc(self):
+        d = super()._desc()
+        d.samples_per_symbol = self._sps
         return d
 
 
@@ -433,11 +490,15 @@ class DigitalModulator:
         self.carrier, self.phasor = carrier, phasor
         self.sps, self.dtype, self.out_mode, self.device = int(samples_per_symbol), dtype, out_mode, device
         self.bps = phasor.bits_per_symbol()
-        self._lut = phasor.lut()
+        sample_dep = getattr(phasor, "sample_dependent", False)
+        self._lut = None if sample_dep else phasor.lut()
         self.taps = None if taps is None else np.ascontiguousarray(taps, dtype=np.float32)
         d = _TxDesc()
         d.bits_per_symbol = self.bps
-        d.lut = _fptr(self._lut)
+        d.lut = _fptr(self._lut) if self._lut is not None else None
+        if sample_dep:
+            self._pdesc = phasor._desc()
+            d.phasor = ctypes.pointer(self._pdesc)
         d.samples_per_symbol = self.sps
         d.taps = _fptr(self.taps) if self.taps is not None else None
         d.ntaps = 0 if self.taps is None else len(self.taps)

@@ -10,8 +10,8 @@
 // modulated data (modulate.rs:128-133), both on one carrier. Panics of the reference (missing
 // or unparsable options, the asserts at modulate.rs:62,68, a non-binary digit on stdin at
 // data.rs:155, an unknown modulation) exit with status 101, as a Rust panic does. The
-// stateful phasors (bfsk, msk, mfsk, 16cpfsk, dcqpsk, dqpsk, dbpsk: SURVEY.md §8f row 3) are
-// not implemented by this backend and exit with status 2.
+// phasors that accumulate phase in f32 from symbol to symbol (bfsk, mfsk, dqpsk, dbpsk:
+// SURVEY.md §8f row 3) are not implemented by this backend and exit with status 2.
 #include "../../include/modem_hip.h"
 
 #include <cmath>
@@ -90,11 +90,25 @@ Opts parse_args(int argc, char** argv) {
     return o;
 }
 
-// The memoryless phasors of modulate.rs:74-95 as LUT descriptors (modem_phasor_lut).
-bool phasor_for(const std::string& m, modem_phasor_desc& d, std::vector<modem_ring>& rings, bool& offset) {
+// The phasors of modulate.rs:74-95 as descriptors: memoryless ones become a LUT
+// (modem_phasor_lut), sample-dependent ones (dcqpsk, msk, 16cpfsk) go to the TX handle as
+// modem_tx_desc.phasor. `offset`: the EvenOddOffset source (modulate.rs:101-107).
+bool phasor_for(const std::string& m, size_t sr, size_t br, size_t sps, modem_phasor_desc& d,
+                std::vector<modem_ring>& rings, bool& offset) {
     std::memset(&d, 0, sizeof d);
     d.amplitude = kAmplitude;
     offset = false;
+    if (m == "dcqpsk") { d.kind = MODEM_PHASOR_DCQPSK; return true; }                  // :86
+    if (m == "msk") {                                                                   // :81
+        if (sps % 2 != 0) panic("assertion failed: samples_per_symbol % 2 == 0");       // msk.rs:14
+        d.kind = MODEM_PHASOR_MSK; d.samples_per_symbol = (uint32_t)sps; offset = true;
+        return true;
+    }
+    if (m == "16cpfsk") {                                                               // :87
+        d.kind = MODEM_PHASOR_CPFSK; d.bits_per_symbol = 4;
+        d.freq = modem_freq_sample_freq(1 * br / 2, sr);                                // cpfsk.rs:20-21
+        return true;
+    }
     if (m == "bask") { d.kind = MODEM_PHASOR_BASK; return true; }
     if (m == "bpsk") { d.kind = MODEM_PHASOR_BPSK; d.phase = kPi / 4.0f; return true; }
     if (m == "qpsk") { d.kind = MODEM_PHASOR_QPSK; d.phase = 0.0f; return true; }
@@ -145,8 +159,8 @@ int main(int argc, char** argv) {
     modem_phasor_desc pd;
     std::vector<modem_ring> rings;
     bool offset = false;
-    if (!phasor_for(o.mod, pd, rings, offset)) {
-        static const char* stateful[] = {"bfsk", "msk", "mfsk", "16cpfsk", "dcqpsk", "dqpsk", "dbpsk"};
+    if (!phasor_for(o.mod, sr, br, sps, pd, rings, offset)) {
+        static const char* stateful[] = {"bfsk", "mfsk", "dqpsk", "dbpsk"};
         for (const char* s : stateful)
             if (o.mod == s) {
                 std::fprintf(stderr, "modulate: '%s' is a stateful phasor, not implemented by the MI355X "
@@ -157,8 +171,10 @@ int main(int argc, char** argv) {
     }
     uint32_t bps = 0;
     check(modem_phasor_bits(&pd, &bps), "phasor");
+    const bool per_sample = pd.kind == MODEM_PHASOR_DCQPSK || pd.kind == MODEM_PHASOR_MSK ||
+                            pd.kind == MODEM_PHASOR_CPFSK;
     std::vector<float> lut(2u << bps);
-    check(modem_phasor_lut(&pd, lut.data()), "phasor");
+    if (!per_sample) check(modem_phasor_lut(&pd, lut.data()), "phasor");
     if (offset && sps % 2 != 0) panic("assertion failed: samples_per_symbol % bits_per_symbol == 0");
 
     uint64_t s0 = 0;                                   // the carrier shared by preamble and data
@@ -197,6 +213,7 @@ int main(int argc, char** argv) {
     d.dtype = MODEM_DTYPE_F32;
     d.out_mode = o.iq ? MODEM_OUT_IQ_BASEBAND : MODEM_OUT_REAL;
     d.q_offset = offset ? (uint32_t)(sps / 2) : 0;
+    d.phasor = per_sample ? &pd : nullptr;
     modem_tx* h = nullptr;
     check(modem_tx_create(&d, 0, &h), "modulator");
 

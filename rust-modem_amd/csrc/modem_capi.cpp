@@ -100,11 +100,16 @@ modem_status phasor_bps(const modem_phasor_desc* d, uint32_t* bps) {
     case MODEM_PHASOR_QAM:
         if (d->bits_per_symbol < 2 || d->bits_per_symbol > 8) return MODEM_ERR_INVALID_ARG;  // qam.rs:17
         *bps = d->bits_per_symbol; return MODEM_OK;
-    case MODEM_PHASOR_MPSK: case MODEM_PHASOR_APSK:
+    case MODEM_PHASOR_MPSK: case MODEM_PHASOR_APSK: case MODEM_PHASOR_CPFSK:
         if (d->bits_per_symbol < 1 || d->bits_per_symbol > 8) return MODEM_ERR_INVALID_ARG;
         *bps = d->bits_per_symbol; return MODEM_OK;
+    case MODEM_PHASOR_DCQPSK: case MODEM_PHASOR_MSK: *bps = 2; return MODEM_OK;   // dcqpsk.rs:39, msk.rs:28
     default: return MODEM_ERR_INVALID_ARG;
     }
+}
+
+bool phasor_sample_dependent(int kind) {
+    return kind == MODEM_PHASOR_DCQPSK || kind == MODEM_PHASOR_CPFSK || kind == MODEM_PHASOR_MSK;
 }
 
 // i(_, b), q(_, b) of one memoryless phasor for the bit slice b (MSB first).
@@ -227,6 +232,7 @@ modem_status modem_phasor_lut(const modem_phasor_desc* d, float* lut) {
     uint32_t bps;
     modem_status st = phasor_bps(d, &bps);
     if (st) return st;
+    if (phasor_sample_dependent(d->kind)) return MODEM_ERR_UNSUPPORTED;   // no bits-only table
     if (d->kind == MODEM_PHASOR_APSK && (st = apsk_verify(d, bps))) return st;
     uint8_t b[8];
     for (uint32_t s = 0; s < (1u << bps); ++s) {
@@ -241,6 +247,7 @@ modem_status modem_phasor_slicer(const modem_phasor_desc* d, const float* lut, m
     uint32_t bps;
     modem_status st = phasor_bps(d, &bps);
     if (st) return st;
+    if (phasor_sample_dependent(d->kind)) return MODEM_ERR_UNSUPPORTED;
     std::memset(o, 0, sizeof *o);
     o->bits_per_symbol = bps;
     if (d->kind == MODEM_PHASOR_QAM && d->phase == 0.0f && bps % 2 == 0 && d->amplitude > 0.0f) {
@@ -292,6 +299,9 @@ struct modem_tx {
     float* d_taps = nullptr;
     float* d_taps_q = nullptr;      // Q-rail taps when q_offset != 0
     uint32_t q_offset = 0;
+    int ph_kind = 0;                // sample-dependent phasor (tx_phasor), else 0
+    float ph_amp = 0.f, ph_freq = 0.f;
+    int ph_spb = 0;
     float2* d_hist[2] = {nullptr, nullptr};
     uint8_t* d_carry[2] = {nullptr, nullptr};
     int hcur = 0, ccur = 0, ncarry = 0;
@@ -319,7 +329,7 @@ static size_t tx_sample_bytes(const modem_tx* h) {
 modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out) {
     if (!d || !out) return MODEM_ERR_INVALID_ARG;
     *out = nullptr;
-    if (d->bits_per_symbol < 1 || d->bits_per_symbol > 8 || !d->lut) return MODEM_ERR_INVALID_ARG;
+    if (d->bits_per_symbol < 1 || d->bits_per_symbol > 8) return MODEM_ERR_INVALID_ARG;
     if (d->samples_per_symbol < 1) return MODEM_ERR_INVALID_ARG;   // SymbolClock % 0 panics (data.rs:29)
     if (d->ntaps > (uint32_t)mk::kMaxTaps || (d->ntaps && !d->taps)) return MODEM_ERR_INVALID_ARG;
     if (d->dtype != MODEM_DTYPE_F32 && d->dtype != MODEM_DTYPE_F16) return MODEM_ERR_INVALID_ARG;
@@ -328,12 +338,42 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     if (d->q_offset != 0 && (d->bits_per_symbol != 2 || d->samples_per_symbol % 2 != 0 ||
                              d->q_offset != d->samples_per_symbol / 2))
         return MODEM_ERR_INVALID_ARG;
+    // Sample-dependent phasors (tx_phasor): sample-and-hold only; the LUT is built here.
+    const modem_phasor_desc* pd = d->phasor;
+    std::vector<float> plut;
+    if (pd) {
+        uint32_t pbps = 0;
+        if (!phasor_sample_dependent(pd->kind) || phasor_bps(pd, &pbps) != MODEM_OK ||
+            pbps != d->bits_per_symbol)
+            return MODEM_ERR_INVALID_ARG;
+        if (d->ntaps != 0) return MODEM_ERR_UNSUPPORTED;
+        if (pd->kind == MODEM_PHASOR_MSK && (pd->samples_per_symbol == 0 || pd->samples_per_symbol % 2))
+            return MODEM_ERR_INVALID_ARG;                                   // msk.rs:14
+        if (d->q_offset && pd->kind != MODEM_PHASOR_MSK) return MODEM_ERR_UNSUPPORTED;
+        if (pd->kind == MODEM_PHASOR_DCQPSK) {                              // dcqpsk.rs:23-36
+            const float map[4] = {0.0f, kPi / 2.0f, 3.0f * kPi / 2.0f, kPi};
+            for (int parity = 0; parity < 2; ++parity)     // even symbol count -> term + pi/4
+                for (int k = 0; k < 4; ++k) {
+                    const float term = parity == 0 ? map[k] + kPi / 4.0f : map[k];
+                    plut.push_back(pd->amplitude * std::cos(term));         // :46-52
+                    plut.push_back(pd->amplitude * std::sin(term));
+                }
+        }
+    } else if (!d->lut) {
+        return MODEM_ERR_INVALID_ARG;
+    }
     if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
     DeviceGuard g(device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     modem_tx* h = new (std::nothrow) modem_tx;
     if (!h) return MODEM_ERR_ALLOC;
     h->device = device;
+    if (pd) {
+        h->ph_kind = pd->kind;
+        h->ph_amp = pd->amplitude;
+        h->ph_freq = pd->freq;
+        h->ph_spb = (int)(pd->samples_per_symbol / 2);
+    }
     h->bps = d->bits_per_symbol;
     h->sps = d->samples_per_symbol;
     h->ntaps = d->ntaps;
@@ -357,7 +397,8 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
         for (uint32_t j = 0; j < L; ++j) pq[(size_t)((j + D) / h->sps) * h->sps + (j + D) % h->sps] = tap(j);
     }
     modem_status st;
-    const size_t nl = (size_t)1 << h->bps;
+    const size_t nl = pd ? std::max<size_t>(1, plut.size() / 2) : (size_t)1 << h->bps;
+    const float* lut_src = pd ? plut.data() : d->lut;
     if ((st = dalloc(&h->d_lut, nl)) || (st = dalloc(&h->d_taps, pp.size())) ||
         (st = dalloc(&h->d_hist[0], h->K)) || (st = dalloc(&h->d_hist[1], h->K)) ||
         (st = dalloc(&h->d_carry[0], 8)) || (st = dalloc(&h->d_carry[1], 8)) ||
@@ -365,7 +406,7 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
         delete h;
         return st;
     }
-    if (hipMemcpy(h->d_lut, d->lut, nl * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess ||
+    if ((lut_src && hipMemcpy(h->d_lut, lut_src, nl * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemcpy(h->d_taps, pp.data(), pp.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
         (D && hipMemcpy(h->d_taps_q, pq.data(), pq.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)) {
         (void)hipGetLastError();
@@ -375,7 +416,7 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     // Sample-and-hold EvenOddOffset: before the first Q tick the phasor sees cur = [b0, 0]
     // (data.rs:84), i.e. the Q value of symbol index 0; it enters as the history symbol that
     // the delayed Q rail reads for n < D (its I value meets zero taps).
-    if (D && d->ntaps == 0 &&
+    if (D && d->ntaps == 0 && !pd &&
         hipMemcpy(h->d_hist[0] + (h->K - 2), d->lut, sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipGetLastError();
         delete h;
@@ -386,7 +427,7 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     const char* env = std::getenv("MODEM_HIP_FIR");
     const bool force_valu = env && std::strcmp(env, "valu") == 0;
     // Sample-and-hold (no taps) stays on the VALU kernels, which reproduce it bit for bit.
-    h->mfma_ksteps = (force_valu || d->ntaps == 0 || D) ? 0 : mk::tx_mfma_ksteps((int)h->sps, (int)h->K);
+    h->mfma_ksteps = (force_valu || d->ntaps == 0 || D || pd) ? 0 : mk::tx_mfma_ksteps((int)h->sps, (int)h->K);
     if (h->mfma_ksteps > 0) {
         // Split-f16 operands of tx_mfma (modem_tx.hip). Exact power-of-two scales put the
         // maxima of the LUT and of the taps in [2^14, 2^15); both are split hi + lo =
@@ -514,7 +555,15 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     p.level_inv = h->level_inv;
     const uint32_t sb = (h->sps <= 16 && 16 % h->sps == 0) ? 16 / h->sps : 1;   // symbols per row-block
     p.lead = (int)(h->symbols % sb);
-    if (h->mfma_ksteps > 0)
+    p.ph_kind = h->ph_kind;
+    p.sym0 = h->symbols;
+    p.ph_amp = h->ph_amp;
+    p.ph_freq = h->ph_freq;
+    p.ph_spb = h->ph_spb;
+    p.q_off = (int)h->q_offset;
+    if (h->ph_kind)
+        HIP_TRY(mk::launch_tx_phasor(p, h->dtype, h->out_mode, s));
+    else if (h->mfma_ksteps > 0)
         HIP_TRY(mk::launch_tx_mfma(p, (int)h->sps, h->mfma_ksteps, h->d_bfrag, h->dtype, h->out_mode, s));
     else
         HIP_TRY(mk::launch_tx(p, (int)h->sps, h->dtype, h->out_mode, s));

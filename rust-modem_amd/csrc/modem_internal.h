@@ -42,6 +42,17 @@ struct TxParams {
     // history maps to the level rint(v * level_inv), level_inv = 1/s.
     int32_t levels;
     float level_inv;
+    // tx_phasor (sample-dependent phasors, sample-and-hold): kind (modem_phasor_kind), the
+    // symbols emitted before this call (DCQPSK parity), amplitude, CPFSK frequency, MSK
+    // samples per bit, Q offset (0 or sps/2). `lut` then holds the DCQPSK table
+    // (even-count block, then odd-count block); `hist[0].x` the index of the symbol before
+    // symbol 0 (the offset Q rail's bits).
+    int32_t ph_kind;
+    uint64_t sym0;
+    float ph_amp;
+    float ph_freq;
+    int32_t ph_spb;
+    int32_t q_off;
 };
 
 // One RX launch: input samples [0, N) (stream indices n_start ..), outputs k_first ..
@@ -87,6 +98,8 @@ struct FirParams {
 // Launchers return hipSuccess or the launch error. They pick a specialised kernel for the
 // common samples-per-symbol values and a generic one otherwise.
 hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s);
+// Sample-dependent phasors (DCQPSK, CPFSK, MSK), sample-and-hold: tx_phasor.
+hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s);
 // TX FIR on the matrix cores (tx_mfma, split-f16 MFMA): 32-symbol k-steps for (sps, K), or 0
 // when no variant fits; bfrag = per-lane B fragments [ksteps][hi, lo][64 lanes][8 halves].
 int tx_mfma_ksteps(int sps, int K);

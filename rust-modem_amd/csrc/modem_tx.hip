@@ -607,6 +607,77 @@ static hipError_t tx_go(const TxParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// ------------------------------------------------------- sample-dependent phasors ----
+// DigitalModulator (modulator.rs:85-100) with a phasor whose (i, q) depend on more than the
+// symbol's bits, one thread per sample, sample-and-hold:
+//   DCQPSK (dcqpsk.rs:23-52): the term alternates between MAP + pi/4 and MAP at every symbol
+//     tick (update() toggles `even` before the first symbol) -> host table of 2 x 4 entries
+//     indexed by the parity of the symbol count since the stream start;
+//   CPFSK (cpfsk.rs:27-45): amp * cos/sin(2*sym * freq * s);
+//   MSK (msk.rs:23-37, over EvenOddOffset when q_off = sps/2): amp * sign(b0) * cos(pi/2*s/spb),
+//     -amp * sign(b1) * sin(pi/2*s/spb);
+// s is the carrier sample index after Carrier::next (sample n -> s0 + n + 1), converted like
+// Rust's `as f32`; f32 operations in the reference's left-to-right order.
+enum { PH_DCQPSK = 8, PH_CPFSK = 10, PH_MSK = 11 };
+
+__device__ __forceinline__ float2 tx_phasor_value(const TxParams& p, int64_t n, int64_t m) {
+#pragma clang fp contract(off)
+    const uint32_t idx = tx_symbol_index(p, m);
+    const float sf = (float)(p.s0 + (uint64_t)n + 1u);
+    if (p.ph_kind == PH_DCQPSK) return p.lut[(((p.sym0 + (uint64_t)m) & 1u) ? 4u : 0u) + idx];
+    if (p.ph_kind == PH_CPFSK) {
+        const float x = (2.0f * (float)idx) * p.ph_freq * sf;
+        float sn, cs;
+        sincosf(x, &sn, &cs);
+        return make_float2(p.ph_amp * cs, p.ph_amp * sn);
+    }
+    // MSK: I bit from this symbol, Q bit from the symbol q_off samples earlier
+    uint32_t qidx = idx;
+    if (p.q_off) {
+        const int64_t mq = (n - p.q_off) >= 0 ? (n - p.q_off) / p.sps : -1;
+        qidx = mq >= 0 ? tx_symbol_index(p, mq) : (uint32_t)p.hist[0].x;
+    }
+    const float x = 1.57079637f * sf / (float)p.ph_spb;          // PI / 2.0 * s / spb
+    float sn, cs;
+    sincosf(x, &sn, &cs);
+    const float si = ((idx >> 1) & 1u) ? 1.0f : -1.0f, sq = (qidx & 1u) ? 1.0f : -1.0f;
+    return make_float2(p.ph_amp * si * cs, -p.ph_amp * sq * sn);
+}
+
+template <int OUT_MODE, typename OutT>
+__global__ __launch_bounds__(256) void tx_phasor(const TxParams p) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        // state for the next call: the last symbol's index (the offset Q rail), leftover bits
+        p.hist_new[0] = p.nsym > 0 ? make_float2((float)tx_symbol_index(p, p.nsym - 1), 0.f) : p.hist[0];
+        if (p.update_carry)
+            for (int i = 0; i < p.ncarry_new; ++i) {
+                const int64_t l = p.nsym * p.bps + i;
+                p.carry_new[i] = l < p.ncarry ? p.carry[l] : p.bits[l - p.ncarry];
+            }
+    }
+    const int64_t nsamp = p.nsym * p.sps;
+    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < nsamp;
+         n += (int64_t)gridDim.x * blockDim.x) {
+        const float2 y = tx_phasor_value(p, n, n / p.sps);
+        tx_emit<OUT_MODE, OutT>(p, n, y, make_float2(0.f, 0.f), false);
+    }
+}
+
+hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s) {
+    const int64_t nsamp = p.nsym * p.sps;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nsamp + 255) / 256, 8192));
+    auto go = [&](auto outt) {
+        using OutT = decltype(outt);
+        switch (out_mode) {
+        case OUT_IQ_MIXED: hipLaunchKernelGGL((tx_phasor<OUT_IQ_MIXED, OutT>), dim3(grid), dim3(256), 0, s, p); break;
+        case OUT_IQ_BASEBAND: hipLaunchKernelGGL((tx_phasor<OUT_IQ_BASEBAND, OutT>), dim3(grid), dim3(256), 0, s, p); break;
+        default: hipLaunchKernelGGL((tx_phasor<OUT_REAL, OutT>), dim3(grid), dim3(256), 0, s, p); break;
+        }
+        return hipGetLastError();
+    };
+    return dtype == 1 ? go(__half()) : go(float());
+}
+
 template <int OM, typename OutT>
 static hipError_t tx_sps(const TxParams& p, int sps, hipStream_t s) {
     switch (p.taps_q ? 0 : sps) {                  // a delayed Q rail: generic kernel

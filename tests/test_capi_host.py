@@ -210,6 +210,7 @@ def test_modulate_cli_argument_panics():
     assert _cli(["-m", "qpsk", "-r", "x"]) == 101           # invalid sample rate
     assert _cli(["-m", "qpsk", "-c", "6000"]) == 101        # cf < sr / 2 (modulate.rs:68)
     assert _cli(["-m", "qpsk", "-c", "900", "-p", "1"]) == 101   # sr % cf == 0 (modulate.rs:62)
-    for s in ("bfsk", "msk", "mfsk", "16cpfsk", "dcqpsk", "dqpsk", "dbpsk"):
+    for s in ("bfsk", "mfsk", "dqpsk", "dbpsk"):
         assert _cli(["-m", s]) == 2
+    assert _cli(["-m", "msk"]) == 101                       # 45 samples/symbol: msk.rs:14
     assert _cli(["-h"]) == 0

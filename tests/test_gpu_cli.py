@@ -14,7 +14,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLI = os.path.join(ROOT, "rust-modem_amd", "bin", "modulate")
-MODS = ["bask", "bpsk", "qpsk", "qam16", "qam256", "16psk", "oqpsk", "16apsk"]
+MODS = ["bask", "bpsk", "qpsk", "qam16", "qam256", "16psk", "oqpsk", "16apsk", "dcqpsk"]
 
 pytestmark = pytest.mark.gpu
 
@@ -52,13 +52,13 @@ def test_cli_iq_bit_exact(o, torch_cuda, mod):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("mod", ["qpsk", "qam16", "oqpsk", "16apsk"])
+@pytest.mark.parametrize("mod", ["qpsk", "qam16", "oqpsk", "16apsk", "msk", "16cpfsk"])
 @pytest.mark.parametrize("pc", [0, 3])
 def test_cli_passband(o, torch_cuda, mod, pc):
     text = bits_text(o, 12, 8 * 200)
     # defaults: -r 10000 -b 220 -c 1000 (45 samples per symbol); EvenOddOffset needs an even
     # count (data.rs:92), so oqpsk runs at 250 baud
-    br = 250 if mod == "oqpsk" else 220
+    br = 250 if mod in ("oqpsk", "msk") else 220
     args = ["-m", mod] + (["-b", str(br)] if br != 220 else []) + (["-p", str(pc)] if pc else [])
     rc, got, err = run_cli(args, text)
     assert rc == 0, err
@@ -75,8 +75,19 @@ def test_cli_bad_digit_panics_after_complete_symbols(o, torch_cuda):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("mod", ["msk", "16cpfsk"])
+def test_cli_iq_sample_dependent(o, torch_cuda, mod):
+    text = bits_text(o, 14, 8 * 300)
+    rc, got, err = run_cli(["-m", mod, "-b", "250", "--iq"], text)
+    assert rc == 0, err
+    ref = oracle_cli(o, mod, 10000, 250, 1000, 0, True, text)
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
 def test_cli_stateful_and_invalid(torch_cuda):
     assert run_cli(["-m", "bfsk"], b"0101")[0] == 2
+    assert run_cli(["-m", "msk"], b"0101")[0] == 101                 # 45 samples/symbol: msk.rs:14
     assert run_cli(["-m", "nope"], b"0101")[0] == 101
     assert run_cli([], b"0101")[0] == 101                            # -m is required
     assert run_cli(["-m", "qpsk", "-c", "6000"], b"0101")[0] == 101   # cf < sr / 2 (modulate.rs:68)
