@@ -96,7 +96,14 @@ typedef enum {
     MODEM_PHASOR_DCQPSK = 8, /* DCQPSK::new(amplitude)                 dcqpsk.rs:16-21 */
     MODEM_PHASOR_CPFSK = 10, /* CPFSK::new(bps, rates, amp, deviation) cpfsk.rs:15-25; freq =
                               * Freq::new(deviation * baud / 2, sr).sample_freq() */
-    MODEM_PHASOR_MSK = 11    /* MSK::new(amplitude, samples_per_symbol) msk.rs:13-21 */
+    MODEM_PHASOR_MSK = 11,   /* MSK::new(amplitude, samples_per_symbol) msk.rs:13-21 */
+    /* Phasors that carry a phase from symbol to symbol in f32 (update() at every symbol
+     * tick): the symbol states are computed by an exact serial scan on the device, then
+     * evaluated per sample; exact, but one stream scans at tens of Msymbols/s. */
+    MODEM_PHASOR_DMPSK = 9,  /* DMPSK::new(bps, amplitude, phase, shift) dmpsk.rs:16-23 */
+    MODEM_PHASOR_MFSK = 12,  /* MFSK::new(bps, deviation, amplitude, map) mfsk.rs:46-59;
+                              * freq = deviation.sample_freq(), mfsk_map 1 = IncreaseMap */
+    MODEM_PHASOR_BFSK = 13   /* BFSK::new(deviation, amplitude)        bfsk.rs:12-20; freq as MFSK */
 } modem_phasor_kind;
 
 typedef struct { uint8_t start, end; float radius, phase; } modem_ring; /* apsk.rs:60-82 */
@@ -108,8 +115,12 @@ typedef struct {
     float amplitude;
     uint32_t nrings;             /* APSK */
     const modem_ring* rings;     /* APSK */
-    float freq;                  /* CPFSK: its sample frequency (cpfsk.rs:20-21) */
+    float freq;                  /* CPFSK: its sample frequency (cpfsk.rs:20-21); MFSK, BFSK:
+                                  * the deviation's sample frequency */
     uint32_t samples_per_symbol; /* MSK: samples per symbol (even, msk.rs:14) */
+    float shift;                 /* DMPSK: phase step per symbol value (dmpsk.rs:20); its
+                                  * initial phase is `phase` */
+    uint32_t mfsk_map;           /* MFSK: 0 = DefaultMap (2s - max), 1 = IncreaseMap (2s) */
 } modem_phasor_desc;
 
 /* Slicer description; fill it with modem_phasor_slicer() or by hand. */

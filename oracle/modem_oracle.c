@@ -225,6 +225,27 @@ int or_msk_new(or_phasor* p, float amplitude, size_t sps) {                  /* 
     p->amplitude = amplitude; p->samples_per_bit = sps / 2; p->bits_per_symbol = 2;
     return 0;
 }
+int or_mfsk_new(or_phasor* p, size_t bps, float deviation, float amplitude, int increase_map) {
+    or_phasor_zero(p, OR_MFSK);                           /* mfsk.rs:46-59 */
+    p->bits_per_symbol = bps; p->freq = deviation; p->amplitude = amplitude;
+    p->increase_map = increase_map; p->max_symbol = (float)or_max_symbol(bps);
+    p->phase = 0.0f; p->cur_coef = 0.0f;                  /* phase_offset, cur_coef */
+    return 0;
+}
+int or_bfsk_new(or_phasor* p, float deviation, float amplitude) {           /* bfsk.rs:12-20 */
+    or_phasor_zero(p, OR_BFSK);
+    p->freq = deviation; p->amplitude = amplitude; p->phase = 0.0f; p->prev = 0;
+    p->bits_per_symbol = 1;
+    return 0;
+}
+static float or_mfsk_coef(const or_phasor* p, uint8_t symbol) {             /* mfsk.rs:22-35 */
+    return p->increase_map ? (float)(2 * (int)symbol)                      /* IncreaseMap */
+                           : (float)(2 * (int)symbol - (int)p->max_symbol);   /* DefaultMap */
+}
+static float or_bfsk_rads(const or_phasor* p, uint64_t s, uint8_t b) {      /* bfsk.rs:26-28 */
+    return (float)b * p->freq * (float)s;
+}
+
 static float or_cpfsk_inner(const or_phasor* p, const uint8_t* b, size_t n, uint64_t s) {
     float coef = 2.0f * (float)or_bytes_to_bits(b, n);   /* cpfsk.rs:27-29 */
     return coef * p->freq * (float)s;                     /* cpfsk.rs:31-33, left to right */
@@ -253,8 +274,17 @@ static float or_dcqpsk_term(const or_phasor* p, uint8_t symbol) {           /* d
 }
 
 void or_phasor_update(or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
-    (void)s;
     if (p->kind == OR_DCQPSK) p->even = !p->even;         /* dcqpsk.rs:42-44 */
+    else if (p->kind == OR_MFSK) {                        /* mfsk.rs:68-75 */
+        float next = or_mfsk_coef(p, or_bytes_to_bits(b, n));
+        p->phase = p->phase + (p->cur_coef - next) * p->freq * (float)s;
+        p->phase = or_mod_trig(p->phase);
+        p->cur_coef = next;
+    } else if (p->kind == OR_BFSK) {                      /* bfsk.rs:42-53 */
+        if (b[0] == p->prev) return;
+        p->phase = or_mod_trig(p->phase + (b[0] == 1 ? -or_bfsk_rads(p, s, 1) : or_bfsk_rads(p, s - 1, 1)));
+        p->prev = b[0];
+    }
     else if (p->kind == OR_DMPSK)                         /* dmpsk.rs:29-33 */
         p->phase = or_mod_trig(p->phase + (float)or_bytes_to_bits(b, n) * p->shift);
 }
@@ -263,6 +293,8 @@ float or_phasor_i(const or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
     switch (p->kind) {
     case OR_CPFSK: return p->amplitude * cosf(or_cpfsk_inner(p, b, n, s));   /* cpfsk.rs:39-41 */
     case OR_MSK: return p->amplitude * or_bit_to_sign(b[0]) * cosf(or_msk_inner(p, s)); /* msk.rs:31-33 */
+    case OR_MFSK: return p->amplitude * cosf(p->cur_coef * p->freq * (float)s + p->phase); /* mfsk.rs:61-63,77-79 */
+    case OR_BFSK: return p->amplitude * cosf(or_bfsk_rads(p, s, b[0]) + p->phase);  /* bfsk.rs:22-24,30-32 */
     case OR_BPSK: return (or_bit_to_sign(b[0]) * p->amplitude) * cosf(p->phase); /* bpsk.rs:17-27 */
     case OR_QPSK: return p->amplitude * (or_bit_to_sign(b[0]) * p->phase_cos -
                                          or_bit_to_sign(b[1]) * p->phase_sin); /* qpsk.rs:23-28 */
@@ -288,6 +320,8 @@ float or_phasor_q(const or_phasor* p, uint64_t s, const uint8_t* b, size_t n) {
     switch (p->kind) {
     case OR_CPFSK: return p->amplitude * sinf(or_cpfsk_inner(p, b, n, s));   /* cpfsk.rs:43-45 */
     case OR_MSK: return -p->amplitude * or_bit_to_sign(b[1]) * sinf(or_msk_inner(p, s)); /* msk.rs:35-37 */
+    case OR_MFSK: return p->amplitude * sinf(p->cur_coef * p->freq * (float)s + p->phase); /* mfsk.rs:81-83 */
+    case OR_BFSK: return p->amplitude * sinf(or_bfsk_rads(p, s, b[0]) + p->phase);  /* bfsk.rs:34-36 */
     case OR_BPSK: return (or_bit_to_sign(b[0]) * p->amplitude) * sinf(p->phase); /* bpsk.rs:29-31 */
     case OR_QPSK: return p->amplitude * (or_bit_to_sign(b[1]) * p->phase_cos +
                                          or_bit_to_sign(b[0]) * p->phase_sin); /* qpsk.rs:30-35 */
@@ -590,7 +624,9 @@ long or_modulate_cli(const char* name, size_t sr, size_t br, size_t cf, size_t p
     else if (!strcmp(name, "dbpsk")) or_dmpsk_new(&p, 1, AMPLITUDE, OR_PI / 4.0f, OR_PI);
     else if (!strcmp(name, "msk")) { if (or_msk_new(&p, AMPLITUDE, sps)) return -1; }    /* :81 */
     else if (!strcmp(name, "16cpfsk")) or_cpfsk_new(&p, 4, br, sr, AMPLITUDE, 1);       /* :87 */
-    else return -2;                                       /* bfsk/mfsk: out of scope */
+    else if (!strcmp(name, "bfsk")) or_bfsk_new(&p, or_freq_sample_freq(200, sr), AMPLITUDE);   /* :77 */
+    else if (!strcmp(name, "mfsk")) or_mfsk_new(&p, 4, or_freq_sample_freq(50, sr), AMPLITUDE, 1); /* :82-83 */
+    else return -2;
 
     or_source bits; memset(&bits, 0, sizeof bits);        /* :98-99 */
     bits.is_ascii = 1; or_ascii_init(&bits.ascii, text, len, sps, p.bits_per_symbol);

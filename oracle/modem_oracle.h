@@ -84,7 +84,7 @@ int      or_even_odd_next(or_even_odd* e, const uint8_t** slice); /* data.rs:102
 /* ---- digital/<x>.rs : DigitalPhasor plugins ---------------------------------------------- */
 enum {
     OR_BPSK = 1, OR_QPSK = 2, OR_QAM = 3, OR_BASK = 4, OR_MPSK = 5, OR_APSK = 6,
-    OR_OQPSK = 7, OR_DCQPSK = 8, OR_DMPSK = 9, OR_CPFSK = 10, OR_MSK = 11,
+    OR_OQPSK = 7, OR_DCQPSK = 8, OR_DMPSK = 9, OR_CPFSK = 10, OR_MSK = 11, OR_MFSK = 12, OR_BFSK = 13,
 };
 typedef struct { uint8_t start, end; float radius, phase; } or_ring;       /* apsk.rs:60-67 */
 typedef struct {
@@ -93,8 +93,11 @@ typedef struct {
     float amplitude, phase, phase_cos, phase_sin, max_symbol, num_symbols, shift;
     int even;                      /* dcqpsk.rs:12 */
     int nrings; or_ring rings[8];  /* apsk.rs:18 */
-    float freq;                    /* cpfsk.rs:10 */
+    float freq;                    /* cpfsk.rs:10; mfsk.rs:39 / bfsk.rs:6 deviation */
     size_t samples_per_bit;        /* msk.rs:8 */
+    float cur_coef;                /* mfsk.rs:43 */
+    int increase_map;              /* mfsk.rs: IncreaseMap (1) or DefaultMap (0) */
+    uint8_t prev;                  /* bfsk.rs:9 */
 } or_phasor;
 /* Constructors mirror the reference `new` functions; return 0 on success, -1 on the
  * reference's assert! failure. */
@@ -111,6 +114,9 @@ int  or_dmpsk_new(or_phasor* p, size_t bps, float amplitude, float phase, float 
 /* CPFSK::new(bps, Rates::new(br, sr), amplitude, deviation)                   cpfsk.rs:15-25 */
 int  or_cpfsk_new(or_phasor* p, size_t bps, size_t br, size_t sr, float amplitude, size_t deviation);
 int  or_msk_new(or_phasor* p, float amplitude, size_t samples_per_symbol);        /* msk.rs:13-21 */
+/* MFSK::new(bps, deviation.sample_freq(), amplitude, map)                       mfsk.rs:46-59 */
+int  or_mfsk_new(or_phasor* p, size_t bps, float deviation, float amplitude, int increase_map);
+int  or_bfsk_new(or_phasor* p, float deviation, float amplitude);                 /* bfsk.rs:12-20 */
 size_t or_phasor_bits_per_symbol(const or_phasor* p);                     /* phasor.rs:2 */
 void   or_phasor_update(or_phasor* p, uint64_t s, const uint8_t* b, size_t len); /* phasor.rs:4 */
 float  or_phasor_i(const or_phasor* p, uint64_t s, const uint8_t* b, size_t len); /* phasor.rs:6 */

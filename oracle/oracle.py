@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "libmodem_oracle.so")
 
 CHANGED, UNCHANGED, FINISHED = 0, 1, 2
-BPSK, QPSK, QAM, BASK, MPSK, APSK, OQPSK, DCQPSK, DMPSK, CPFSK, MSK = range(1, 12)
+BPSK, QPSK, QAM, BASK, MPSK, APSK, OQPSK, DCQPSK, DMPSK, CPFSK, MSK, MFSK, BFSK = range(1, 14)
 SLICER_NEAREST, SLICER_QAM_AXIS = 0, 1
 MIX_COMPLEX, MIX_REFERENCE_REAL = 0, 1
 OUT_IQ_MIXED, OUT_IQ_BASEBAND, OUT_REAL = 0, 1, 2
@@ -35,7 +35,8 @@ class Phasor(ctypes.Structure):
                 ("phase", ctypes.c_float), ("phase_cos", ctypes.c_float), ("phase_sin", ctypes.c_float),
                 ("max_symbol", ctypes.c_float), ("num_symbols", ctypes.c_float), ("shift", ctypes.c_float),
                 ("even", ctypes.c_int), ("nrings", ctypes.c_int), ("rings", Ring * 8),
-                ("freq", ctypes.c_float), ("samples_per_bit", ctypes.c_size_t)]
+                ("freq", ctypes.c_float), ("samples_per_bit", ctypes.c_size_t),
+                ("cur_coef", ctypes.c_float), ("increase_map", ctypes.c_int), ("prev", ctypes.c_uint8)]
 
 
 class SymbolClock(ctypes.Structure):
@@ -109,6 +110,7 @@ def lib():
         "or_oqpsk_new": (i, [P(Phasor), f]), "or_dcqpsk_new": (i, [P(Phasor), f]),
         "or_dmpsk_new": (i, [P(Phasor), sz, f, f, f]),
         "or_cpfsk_new": (i, [P(Phasor), sz, sz, sz, f, sz]), "or_msk_new": (i, [P(Phasor), f, sz]),
+        "or_mfsk_new": (i, [P(Phasor), sz, f, f, i]), "or_bfsk_new": (i, [P(Phasor), f, f]),
         "or_phasor_update": (None, [P(Phasor), u64, vp, sz]),
         "or_phasor_i": (f, [P(Phasor), u64, vp, sz]), "or_phasor_q": (f, [P(Phasor), u64, vp, sz]),
         "or_fir_block": (None, [fp, sz, fp, sz, fp]),
@@ -171,7 +173,7 @@ def new_phasor(kind: int, *args) -> Phasor:
     L = lib()
     ctor = {BPSK: L.or_bpsk_new, QPSK: L.or_qpsk_new, QAM: L.or_qam_new, BASK: L.or_bask_new,
             MPSK: L.or_mpsk_new, OQPSK: L.or_oqpsk_new, DCQPSK: L.or_dcqpsk_new, DMPSK: L.or_dmpsk_new,
-            CPFSK: L.or_cpfsk_new, MSK: L.or_msk_new}
+            CPFSK: L.or_cpfsk_new, MSK: L.or_msk_new, MFSK: L.or_mfsk_new, BFSK: L.or_bfsk_new}
     if kind == APSK:
         amplitude, bps, rings = args
         arr = (Ring * len(rings))(*[Ring(a, b, r, ph) for (a, b, r, ph) in rings])

@@ -79,7 +79,8 @@ class _PhasorDesc(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("bits_per_symbol", ctypes.c_uint32),
                 ("phase", ctypes.c_float), ("amplitude", ctypes.c_float),
                 ("nrings", ctypes.c_uint32), ("rings", ctypes.POINTER(_Ring)),
-                ("freq", ctypes.c_float), ("samples_per_symbol", ctypes.c_uint32)]
+                ("freq", ctypes.c_float), ("samples_per_symbol", ctypes.c_uint32),
+                ("shift", ctypes.c_float), ("mfsk_map", ctypes.c_uint32)]
 
 
 class _SlicerDesc(ctypes.Structure):
@@ -415,6 +416,49 @@ class MSK(_SamplePhasor):
     def _desc(self):
         d = super()._desc()
         d.samples_per_symbol = self._sps
+        return d
+
+
+class DMPSK(_SamplePhasor):
+    """dmpsk.rs:7-43: DMPSK::new(bits_per_symbol, amplitude, phase, shift); the phase is carried
+    in f32 from symbol to symbol (a serial scan on the device)."""
+    _kind = 9
+
+    def __init__(self, bits_per_symbol: int, amplitude: float, phase: float, shift: float):
+        self._bps, self.amplitude, self._phase, self._shift = int(bits_per_symbol), float(amplitude), \
+            float(phase), float(shift)
+
+    def _desc(self):
+        d = super()._desc()
+        d.shift = self._shift
+        return d
+
+
+class MFSK(_SamplePhasor):
+    """mfsk.rs:37-85: MFSK::new(bits_per_symbol, deviation: Freq, amplitude, map);
+    map "increase" (IncreaseMap, 2s) or "default" (DefaultMap, 2s - max_symbol)."""
+    _kind = 12
+
+    def __init__(self, bits_per_symbol: int, deviation: "Freq", amplitude: float, map: str = "default"):
+        self._bps, self.amplitude = int(bits_per_symbol), float(amplitude)
+        self._freq, self._map = deviation.sample_freq(), 1 if map == "increase" else 0
+
+    def _desc(self):
+        d = super()._desc()
+        d.freq, d.mfsk_map = self._freq, self._map
+        return d
+
+
+class BFSK(_SamplePhasor):
+    """bfsk.rs:4-56: BFSK::new(deviation: Freq, amplitude)."""
+    _kind = 13
+
+    def __init__(self, deviation: "Freq", amplitude: float):
+        self.amplitude, self._freq = float(amplitude), deviation.sample_freq()
+
+    def _desc(self):
+        d = super()._desc()
+        d.freq = self._freq
         return d
 
 

@@ -9,9 +9,8 @@
 // sr/cf*pc - 1 samples of the Raw phasor (modulate.rs:118-126) then the real part of the
 // modulated data (modulate.rs:128-133), both on one carrier. Panics of the reference (missing
 // or unparsable options, the asserts at modulate.rs:62,68, a non-binary digit on stdin at
-// data.rs:155, an unknown modulation) exit with status 101, as a Rust panic does. The
-// phasors that accumulate phase in f32 from symbol to symbol (bfsk, mfsk, dqpsk, dbpsk:
-// SURVEY.md §8f row 3) are not implemented by this backend and exit with status 2.
+// data.rs:155, an unknown modulation) exit with status 101, as a Rust panic does. Every
+// modulation of modulate.rs:74-95 is supported.
 #include "../../include/modem_hip.h"
 
 #include <cmath>
@@ -109,6 +108,17 @@ bool phasor_for(const std::string& m, size_t sr, size_t br, size_t sps, modem_ph
         d.freq = modem_freq_sample_freq(1 * br / 2, sr);                                // cpfsk.rs:20-21
         return true;
     }
+    if (m == "bfsk") { d.kind = MODEM_PHASOR_BFSK; d.freq = modem_freq_sample_freq(200, sr); return true; } // :77
+    if (m == "mfsk") {                                                                  // :82-83
+        d.kind = MODEM_PHASOR_MFSK; d.bits_per_symbol = 4; d.freq = modem_freq_sample_freq(50, sr);
+        d.mfsk_map = 1;                                                                 // IncreaseMap
+        return true;
+    }
+    if (m == "dqpsk" || m == "dbpsk") {                                                 // :92-93
+        d.kind = MODEM_PHASOR_DMPSK; d.bits_per_symbol = m == "dqpsk" ? 2 : 1;
+        d.phase = kPi / 4.0f; d.shift = m == "dqpsk" ? kPi / 2.0f : kPi;
+        return true;
+    }
     if (m == "bask") { d.kind = MODEM_PHASOR_BASK; return true; }
     if (m == "bpsk") { d.kind = MODEM_PHASOR_BPSK; d.phase = kPi / 4.0f; return true; }
     if (m == "qpsk") { d.kind = MODEM_PHASOR_QPSK; d.phase = 0.0f; return true; }
@@ -159,20 +169,13 @@ int main(int argc, char** argv) {
     modem_phasor_desc pd;
     std::vector<modem_ring> rings;
     bool offset = false;
-    if (!phasor_for(o.mod, sr, br, sps, pd, rings, offset)) {
-        static const char* stateful[] = {"bfsk", "mfsk", "dqpsk", "dbpsk"};
-        for (const char* s : stateful)
-            if (o.mod == s) {
-                std::fprintf(stderr, "modulate: '%s' is a stateful phasor, not implemented by the MI355X "
-                                     "backend (SURVEY.md §8f row 3)\n", s);
-                return 2;
-            }
+    if (!phasor_for(o.mod, sr, br, sps, pd, rings, offset))
         panic("invalid digital modulation");                                            // modulate.rs:94
-    }
     uint32_t bps = 0;
     check(modem_phasor_bits(&pd, &bps), "phasor");
     const bool per_sample = pd.kind == MODEM_PHASOR_DCQPSK || pd.kind == MODEM_PHASOR_MSK ||
-                            pd.kind == MODEM_PHASOR_CPFSK;
+                            pd.kind == MODEM_PHASOR_CPFSK || pd.kind == MODEM_PHASOR_DMPSK ||
+                            pd.kind == MODEM_PHASOR_MFSK || pd.kind == MODEM_PHASOR_BFSK;
     std::vector<float> lut(2u << bps);
     if (!per_sample) check(modem_phasor_lut(&pd, lut.data()), "phasor");
     if (offset && sps % 2 != 0) panic("assertion failed: samples_per_symbol % bits_per_symbol == 0");

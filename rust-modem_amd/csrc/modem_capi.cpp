@@ -100,16 +100,22 @@ modem_status phasor_bps(const modem_phasor_desc* d, uint32_t* bps) {
     case MODEM_PHASOR_QAM:
         if (d->bits_per_symbol < 2 || d->bits_per_symbol > 8) return MODEM_ERR_INVALID_ARG;  // qam.rs:17
         *bps = d->bits_per_symbol; return MODEM_OK;
-    case MODEM_PHASOR_MPSK: case MODEM_PHASOR_APSK: case MODEM_PHASOR_CPFSK:
+    case MODEM_PHASOR_MPSK: case MODEM_PHASOR_APSK: case MODEM_PHASOR_CPFSK: case MODEM_PHASOR_DMPSK:
+    case MODEM_PHASOR_MFSK:
         if (d->bits_per_symbol < 1 || d->bits_per_symbol > 8) return MODEM_ERR_INVALID_ARG;
         *bps = d->bits_per_symbol; return MODEM_OK;
     case MODEM_PHASOR_DCQPSK: case MODEM_PHASOR_MSK: *bps = 2; return MODEM_OK;   // dcqpsk.rs:39, msk.rs:28
+    case MODEM_PHASOR_BFSK: *bps = 1; return MODEM_OK;                            // bfsk.rs:23
     default: return MODEM_ERR_INVALID_ARG;
     }
 }
 
+bool phasor_scanned(int kind) {          // phase carried from symbol to symbol (tx_scan)
+    return kind == MODEM_PHASOR_DMPSK || kind == MODEM_PHASOR_MFSK || kind == MODEM_PHASOR_BFSK;
+}
 bool phasor_sample_dependent(int kind) {
-    return kind == MODEM_PHASOR_DCQPSK || kind == MODEM_PHASOR_CPFSK || kind == MODEM_PHASOR_MSK;
+    return kind == MODEM_PHASOR_DCQPSK || kind == MODEM_PHASOR_CPFSK || kind == MODEM_PHASOR_MSK ||
+           phasor_scanned(kind);
 }
 
 // i(_, b), q(_, b) of one memoryless phasor for the bit slice b (MSB first).
@@ -300,8 +306,9 @@ struct modem_tx {
     float* d_taps_q = nullptr;      // Q-rail taps when q_offset != 0
     uint32_t q_offset = 0;
     int ph_kind = 0;                // sample-dependent phasor (tx_phasor), else 0
-    float ph_amp = 0.f, ph_freq = 0.f;
-    int ph_spb = 0;
+    float ph_amp = 0.f, ph_freq = 0.f, ph_shift = 0.f, ph_max = 0.f;
+    int ph_spb = 0, ph_map = 0;
+    Stage scan_stage;               // per-symbol states of the scanned phasors
     float2* d_hist[2] = {nullptr, nullptr};
     uint8_t* d_carry[2] = {nullptr, nullptr};
     int hcur = 0, ccur = 0, ncarry = 0;
@@ -373,6 +380,9 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
         h->ph_amp = pd->amplitude;
         h->ph_freq = pd->freq;
         h->ph_spb = (int)(pd->samples_per_symbol / 2);
+        h->ph_shift = pd->shift;
+        h->ph_map = pd->mfsk_map ? 1 : 0;
+        h->ph_max = (float)((1u << d->bits_per_symbol) - 1u);                 // max_symbol, util.rs:13-15
     }
     h->bps = d->bits_per_symbol;
     h->sps = d->samples_per_symbol;
@@ -416,6 +426,15 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     // Sample-and-hold EvenOddOffset: before the first Q tick the phasor sees cur = [b0, 0]
     // (data.rs:84), i.e. the Q value of symbol index 0; it enters as the history symbol that
     // the delayed Q rail reads for n < D (its I value meets zero taps).
+    // DMPSK starts from its phase (dmpsk.rs:20); MFSK / BFSK from zeros (mfsk.rs:55-56, bfsk.rs:16-17)
+    if (pd && pd->kind == MODEM_PHASOR_DMPSK) {
+        const float2 st0 = make_float2(pd->phase, 0.0f);
+        if (hipMemcpy(h->d_hist[0], &st0, sizeof st0, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipGetLastError();
+            delete h;
+            return MODEM_ERR_HIP;
+        }
+    }
     if (D && d->ntaps == 0 && !pd &&
         hipMemcpy(h->d_hist[0] + (h->K - 2), d->lut, sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipGetLastError();
@@ -561,6 +580,14 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     p.ph_freq = h->ph_freq;
     p.ph_spb = h->ph_spb;
     p.q_off = (int)h->q_offset;
+    p.ph_shift = h->ph_shift;
+    p.ph_map = h->ph_map;
+    p.ph_max = h->ph_max;
+    p.scan = nullptr;
+    if (phasor_scanned(h->ph_kind)) {
+        if ((st = h->scan_stage.ensure((size_t)std::max<int64_t>(nsym, 1) * sizeof(float2)))) return st;
+        p.scan = static_cast<float2*>(h->scan_stage.p);
+    }
     if (h->ph_kind)
         HIP_TRY(mk::launch_tx_phasor(p, h->dtype, h->out_mode, s));
     else if (h->mfma_ksteps > 0)

@@ -53,6 +53,13 @@ struct TxParams {
     float ph_freq;
     int32_t ph_spb;
     int32_t q_off;
+    // DMPSK / MFSK / BFSK: per-symbol states of this call (tx_scan writes, tx_phasor reads),
+    // the DMPSK shift, the MFSK map and max symbol. The handle state (DMPSK phase; MFSK
+    // cur_coef, phase_offset; BFSK phase, prev bit) is hist[0] -> hist_new[0].
+    float2* scan;
+    float ph_shift;
+    int32_t ph_map;
+    float ph_max;
 };
 
 // One RX launch: input samples [0, N) (stream indices n_start ..), outputs k_first ..
@@ -98,7 +105,8 @@ struct FirParams {
 // Launchers return hipSuccess or the launch error. They pick a specialised kernel for the
 // common samples-per-symbol values and a generic one otherwise.
 hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s);
-// Sample-dependent phasors (DCQPSK, CPFSK, MSK), sample-and-hold: tx_phasor.
+// Sample-dependent phasors (DCQPSK, CPFSK, MSK; DMPSK, MFSK, BFSK after a serial symbol-state
+// scan), sample-and-hold: tx_scan + tx_phasor.
 hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s);
 // TX FIR on the matrix cores (tx_mfma, split-f16 MFMA): 32-symbol k-steps for (sps, K), or 0
 // when no variant fits; bfrag = per-lane B fragments [ksteps][hi, lo][64 lanes][8 halves].

@@ -618,13 +618,77 @@ static hipError_t tx_go(const TxParams& p, hipStream_t s) {
 //     -amp * sign(b1) * sin(pi/2*s/spb);
 // s is the carrier sample index after Carrier::next (sample n -> s0 + n + 1), converted like
 // Rust's `as f32`; f32 operations in the reference's left-to-right order.
-enum { PH_DCQPSK = 8, PH_CPFSK = 10, PH_MSK = 11 };
+enum { PH_DCQPSK = 8, PH_DMPSK = 9, PH_CPFSK = 10, PH_MSK = 11, PH_MFSK = 12, PH_BFSK = 13 };
+
+// mod_trig (util.rs:3-6) with the IEEE quotient, for any finite f32 (the scan's phases can be
+// negative, where the carrier's shortcut is not proven).
+__device__ __forceinline__ float mod_trig_ieee(float x) {
+#pragma clang fp contract(off)
+    return x - kTwoPi * __builtin_floorf(x / kTwoPi);
+}
+
+// DMPSK / MFSK / BFSK: update() runs at every symbol tick (modulator.rs:90-93) with the
+// phase carried in f32 from symbol to symbol, so the states are a serial recurrence. One
+// workgroup: its lanes decode 256 symbol indices at a time into LDS, lane 0 runs the
+// recurrence exactly as the reference does, and the lanes write the states out.
+//   DMPSK (dmpsk.rs:29-33): phase = mod_trig(phase + sym * shift)
+//   MFSK (mfsk.rs:68-75):   off = mod_trig(off + (cur - next) * dev * s); cur = next
+//   BFSK (bfsk.rs:42-53):   on a change of bit, phase = mod_trig(phase + (b ? -dev*s : dev*(s-1)))
+// s is the carrier sample index after Carrier::next at the symbol's first sample.
+__global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
+#pragma clang fp contract(off)
+    __shared__ uint32_t sidx[256];
+    __shared__ float2 sst[256];
+    float2 st = p.hist[0];
+    for (int64_t base = 0; base < p.nsym; base += 256) {
+        const int64_t m = base + threadIdx.x;
+        if (m < p.nsym) sidx[threadIdx.x] = tx_symbol_index(p, m);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int cnt = (int)(p.nsym - base < 256 ? p.nsym - base : 256);
+            for (int j = 0; j < cnt; ++j) {
+                const uint32_t idx = sidx[j];
+                const uint64_t su = p.s0 + (uint64_t)(base + j) * (uint64_t)p.sps + 1u;
+                if (p.ph_kind == PH_DMPSK) {
+                    st.x = mod_trig_ieee(st.x + (float)idx * p.ph_shift);
+                } else if (p.ph_kind == PH_MFSK) {
+                    const float next = p.ph_map ? (float)(2 * (int)idx) : (float)(2 * (int)idx - (int)p.ph_max);
+                    st.y = st.y + (st.x - next) * p.ph_freq * (float)su;
+                    st.y = mod_trig_ieee(st.y);
+                    st.x = next;
+                } else {                                   // BFSK: st = (phase, prev bit)
+                    const float b = (float)(idx & 1u);
+                    if (b != st.y) {
+                        const float d = b == 1.0f ? -(p.ph_freq * (float)su) : p.ph_freq * (float)(su - 1u);
+                        st.x = mod_trig_ieee(st.x + d);
+                        st.y = b;
+                    }
+                }
+                sst[j] = st;
+            }
+        }
+        __syncthreads();
+        if (m < p.nsym) p.scan[m] = sst[threadIdx.x];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) p.hist_new[0] = st;
+}
 
 __device__ __forceinline__ float2 tx_phasor_value(const TxParams& p, int64_t n, int64_t m) {
 #pragma clang fp contract(off)
     const uint32_t idx = tx_symbol_index(p, m);
     const float sf = (float)(p.s0 + (uint64_t)n + 1u);
     if (p.ph_kind == PH_DCQPSK) return p.lut[(((p.sym0 + (uint64_t)m) & 1u) ? 4u : 0u) + idx];
+    if (p.ph_kind == PH_DMPSK || p.ph_kind == PH_MFSK || p.ph_kind == PH_BFSK) {
+        const float2 st = p.scan[m];
+        float x;
+        if (p.ph_kind == PH_DMPSK) x = st.x;                                  // dmpsk.rs:35-41
+        else if (p.ph_kind == PH_MFSK) x = st.x * p.ph_freq * sf + st.y;      // mfsk.rs:61-63
+        else x = (float)(idx & 1u) * p.ph_freq * sf + st.x;                   // bfsk.rs:22-28
+        float sn, cs;
+        sincosf(x, &sn, &cs);
+        return make_float2(p.ph_amp * cs, p.ph_amp * sn);
+    }
     if (p.ph_kind == PH_CPFSK) {
         const float x = (2.0f * (float)idx) * p.ph_freq * sf;
         float sn, cs;
@@ -647,8 +711,10 @@ __device__ __forceinline__ float2 tx_phasor_value(const TxParams& p, int64_t n, 
 template <int OUT_MODE, typename OutT>
 __global__ __launch_bounds__(256) void tx_phasor(const TxParams p) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // state for the next call: the last symbol's index (the offset Q rail), leftover bits
-        p.hist_new[0] = p.nsym > 0 ? make_float2((float)tx_symbol_index(p, p.nsym - 1), 0.f) : p.hist[0];
+        // state for the next call: the last symbol's index (the offset Q rail; the scanned
+        // phasors' state comes from tx_scan), leftover bits
+        if (p.scan == nullptr)
+            p.hist_new[0] = p.nsym > 0 ? make_float2((float)tx_symbol_index(p, p.nsym - 1), 0.f) : p.hist[0];
         if (p.update_carry)
             for (int i = 0; i < p.ncarry_new; ++i) {
                 const int64_t l = p.nsym * p.bps + i;
@@ -665,6 +731,11 @@ __global__ __launch_bounds__(256) void tx_phasor(const TxParams p) {
 
 hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s) {
     const int64_t nsamp = p.nsym * p.sps;
+    if (p.scan != nullptr) {
+        hipLaunchKernelGGL(tx_scan, dim3(1), dim3(256), 0, s, p);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((nsamp + 255) / 256, 8192));
     auto go = [&](auto outt) {
         using OutT = decltype(outt);

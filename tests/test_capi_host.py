@@ -204,13 +204,11 @@ def _cli(args, stdin=b"0101"):
 
 
 def test_modulate_cli_argument_panics():
-    """modulate.rs panics (exit 101) before any device work; stateful phasors exit 2."""
+    """modulate.rs panics (exit 101) before any device work."""
     assert _cli([]) == 101                                  # -m is required (modulate.rs:42)
     assert _cli(["-m", "nope"]) == 101                      # modulate.rs:94
     assert _cli(["-m", "qpsk", "-r", "x"]) == 101           # invalid sample rate
     assert _cli(["-m", "qpsk", "-c", "6000"]) == 101        # cf < sr / 2 (modulate.rs:68)
     assert _cli(["-m", "qpsk", "-c", "900", "-p", "1"]) == 101   # sr % cf == 0 (modulate.rs:62)
-    for s in ("bfsk", "mfsk", "dqpsk", "dbpsk"):
-        assert _cli(["-m", s]) == 2
     assert _cli(["-m", "msk"]) == 101                       # 45 samples/symbol: msk.rs:14
     assert _cli(["-h"]) == 0

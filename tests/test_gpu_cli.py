@@ -3,7 +3,7 @@ oracle's restatement of src/bin/modulate.rs (or_modulate_cli) on the same stdin.
 
 --iq output: bit-exact. Passband output (real part, with and without the preamble): within the
 f32 sample tolerance (hardware sin/cos vs glibc). Panics of the reference exit with 101 after
-the samples of the symbols before the bad digit; stateful phasors exit with 2.
+the samples of the symbols before the bad digit.
 """
 import ctypes
 import os
@@ -75,7 +75,7 @@ def test_cli_bad_digit_panics_after_complete_symbols(o, torch_cuda):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("mod", ["msk", "16cpfsk"])
+@pytest.mark.parametrize("mod", ["msk", "16cpfsk", "bfsk", "mfsk", "dqpsk", "dbpsk"])
 def test_cli_iq_sample_dependent(o, torch_cuda, mod):
     text = bits_text(o, 14, 8 * 300)
     rc, got, err = run_cli(["-m", mod, "-b", "250", "--iq"], text)
@@ -86,7 +86,6 @@ def test_cli_iq_sample_dependent(o, torch_cuda, mod):
 
 
 def test_cli_stateful_and_invalid(torch_cuda):
-    assert run_cli(["-m", "bfsk"], b"0101")[0] == 2
     assert run_cli(["-m", "msk"], b"0101")[0] == 101                 # 45 samples/symbol: msk.rs:14
     assert run_cli(["-m", "nope"], b"0101")[0] == 101
     assert run_cli([], b"0101")[0] == 101                            # -m is required

@@ -1,10 +1,14 @@
-"""Phasors whose (i, q) depend on the symbol count or the sample index:
-DCQPSK (dcqpsk.rs), CPFSK (cpfsk.rs), MSK over EvenOddOffset (msk.rs + data.rs:81-123), on
-the GPU's per-sample phasor kernel (tx_phasor) against the oracle's DigitalModulator
-(modulator.rs:85-100, which passes the post-increment carrier sample to the phasor).
+"""Phasors whose (i, q) depend on the symbol count, the sample index or a phase carried from
+symbol to symbol: DCQPSK (dcqpsk.rs), CPFSK (cpfsk.rs), MSK over
+EvenOddOffset (msk.rs + data.rs:81-123), DMPSK (dmpsk.rs), MFSK (mfsk.rs), BFSK (bfsk.rs), on
+the GPU's per-sample phasor kernel (tx_phasor; the last three after the serial state scan
+tx_scan) against the oracle's DigitalModulator (modulator.rs:85-100, which passes the
+post-increment carrier sample to the phasor).
 
 DCQPSK's values come from a host table built with the reference's f32 formulas: bit-exact.
-CPFSK and MSK take sin/cos of a per-sample argument: the f32 sample tolerance.
+The others take sin/cos of a per-sample argument: the f32 sample tolerance. The scanned
+phases must follow the reference's f32 rounding exactly — long streams (20 000 symbols, where
+a phase that drifted by an ulp per step would be off by far more than the tolerance) check it.
 """
 import ctypes
 
@@ -87,3 +91,34 @@ def test_msk_even_odd(m, o, torch_cuda, sps):
                    chunks=[1, 2, 3, 500, len(bits) - 506])
     one = _gpu(m, torch_cuda, m.MSK(1.0, sps), bits, sps, 0, w, offset=True)
     assert np.array_equal(chunked.view(np.uint32), one.view(np.uint32))
+
+
+SCANNED = {
+    "dqpsk": (lambda m: m.DMPSK(2, 1.0, 0.7853982, 1.5707964),
+              lambda o: o.new_phasor(o.DMPSK, 2, 1.0, 0.7853982, 1.5707964), 2),
+    "dbpsk": (lambda m: m.DMPSK(1, 1.0, 0.7853982, 3.1415927),
+              lambda o: o.new_phasor(o.DMPSK, 1, 1.0, 0.7853982, 3.1415927), 1),
+    "mfsk": (lambda m: m.MFSK(4, m.Freq(50, 10000), 1.0, "increase"),
+             lambda o: o.new_phasor(o.MFSK, 4, o.sample_freq(50, 10000), 1.0, 1), 4),
+    "mfsk_default": (lambda m: m.MFSK(3, m.Freq(120, 10000), 0.5, "default"),
+                     lambda o: o.new_phasor(o.MFSK, 3, o.sample_freq(120, 10000), 0.5, 0), 3),
+    "bfsk": (lambda m: m.BFSK(m.Freq(200, 10000), 1.0),
+             lambda o: o.new_phasor(o.BFSK, o.sample_freq(200, 10000), 1.0), 1),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SCANNED))
+def test_scanned_phasors(m, o, torch_cuda, name):
+    mk, ok, bps = SCANNED[name]
+    sps = 4
+    bits = o.prng_bits(SEED + 4, bps * 20000 + 1)
+    w = o.sample_freq(1000, 10000)
+    got = _gpu(m, torch_cuda, mk(m), bits, sps, 3, w, out_mode=1)
+    ref = o.tx_chain(ok(o), bits, sps, None, w, 3, out_mode=o.OUT_IQ_BASEBAND)
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+    # the state carries across calls (the scan resumes from the handle's state)
+    chunked = _gpu(m, torch_cuda, mk(m), bits, sps, 3, w, out_mode=1,
+                   chunks=[bps * 3 + 1, 0, bps * 7000, len(bits) - bps * 7003 - 1])
+    assert np.array_equal(chunked.view(np.uint32), got.view(np.uint32))
