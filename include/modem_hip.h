@@ -211,6 +211,8 @@ typedef struct {
     int32_t in_dtype;            /* modem_dtype of the input I/Q samples */
     int32_t out_dtype;           /* modem_dtype of the decimated I/Q output */
     modem_slicer_desc slicer;    /* decisions (kind NONE for none) */
+    float phase_offset;          /* PLL::phase_offset added to every carrier phase
+                                  * (demodulator.rs:50); 0 = unlocked. See modem_pll_lock. */
 } modem_rx_desc;
 
 modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out);
@@ -224,6 +226,13 @@ modem_status modem_rx_flush(modem_rx* h, void* out_iq, uint8_t* out_sym, size_t 
                             size_t* produced, void* stream);
 uint64_t modem_rx_sample(const modem_rx* h);
 modem_status modem_rx_destroy(modem_rx* h);
+
+/* Demodulator::lock_phase (demodulator.rs:32-36): PLL::handle (pll.rs:16-22) over the n
+ * complex samples x_iq (host memory; the reference uses n = 64), with the carrier phases of
+ * samples s0 .. s0+n-1, starting from *phase_offset (0 for a new PLL). Control logic over a
+ * few serial samples: evaluated on the host with the reference's f32 operations. */
+modem_status modem_pll_lock(float sample_freq, uint64_t s0, const float* x_iq, size_t n,
+                            float* phase_offset);
 
 /* ---- FIRFilter: real-valued causal FIR over a stream (fir.rs:3-35) ---------------------- */
 typedef struct modem_fir modem_fir;

@@ -437,6 +437,29 @@ void or_demodulate(float sf, uint64_t s0, float phase_offset, const float* taps,
     or_fir_free(&lpi); or_fir_free(&lpq);
 }
 
+size_t or_demodulate_front(float sf, const float* x, size_t n, const float* hil, size_t nh,
+                           const float* lp, size_t nlp, float* out_i, float* out_q, float* off_out) {
+    if (n < 64) return 0;                                 /* lock_phase's unwrap (demodulator.rs:34) */
+    or_fir hf; or_fir_init(&hf, hil, nh);                 /* demodulate.rs:31-34 */
+    or_carrier c; or_carrier_init(&c, sf, 0);             /* demodulate.rs:36-38 */
+    or_pll pll = { 0.0f };
+    or_fir lpi, lpq; or_fir_init(&lpi, lp, nlp); or_fir_init(&lpq, lp, nlp);
+    for (size_t k = 0; k < 64; k++) {                     /* lock_phase, demodulator.rs:32-36 */
+        float im = or_fir_add(&hf, x[k]);
+        or_pll_handle(&pll, or_carrier_next(&c), x[k], im);
+    }
+    size_t m = 0;
+    for (size_t k = 64; k < n; k++, m++) {                /* demodulator.rs:44-56 */
+        (void)or_fir_add(&hf, x[k]);                      /* the analytic map runs for every sample */
+        float phase = or_carrier_next(&c) + pll.phase_offset;
+        out_i[m] = 2.0f * or_fir_add(&lpi, x[k] * cosf(phase));
+        out_q[m] = 2.0f * or_fir_add(&lpq, x[k] * -sinf(phase));
+    }
+    if (off_out) *off_out = pll.phase_offset;
+    or_fir_free(&hf); or_fir_free(&lpi); or_fir_free(&lpq);
+    return m;
+}
+
 /* ---- GLUE ----------------------------------------------------------------------------------- */
 uint64_t or_splitmix64_next(uint64_t* state) {
     uint64_t z = (*state += 0x9E3779B97F4A7C15ULL);

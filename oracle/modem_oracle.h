@@ -151,6 +151,14 @@ void  or_demodulate(float sample_freq, uint64_t s0, float phase_offset,
                     const float* taps, size_t ntaps,
                     const float* x_re, size_t n, float* out_i, float* out_q);
 
+/* demodulate.rs:29-43 with the filters as arguments (the binary hard-codes a 23-tap Hilbert and
+ * a 64-tap low-pass, demodulate.rs:47-150): analytic = (x, hilbert.add(x)) per sample,
+ * Demodulator::new(Carrier::new(freq), analytic, lowpass), lock_phase() (64 samples through the
+ * PLL, demodulator.rs:32-36), then Demodulator::next for every remaining sample. Returns the
+ * outputs written (n - 64; 0 if n < 64, where the reference's unwrap panics). */
+size_t or_demodulate_front(float sample_freq, const float* x, size_t n, const float* hilbert, size_t nh,
+                           const float* lowpass, size_t nlp, float* out_i, float* out_q, float* phase_offset);
+
 /* ---- GLUE (absent from the reference; build-defined, parity unpinned by the reference) --- */
 uint64_t or_splitmix64_next(uint64_t* state);
 /* nbits bits, one byte per bit (data.rs:36 layout): bit i = (word[i/64] >> (i%64)) & 1 */

@@ -122,6 +122,7 @@ def lib():
         "or_tx_chain": (sz, [P(Phasor), vp, sz, sz, fp, sz, f, u64, sz, i, fp]),
         "or_tx_chain_src": (sz, [P(Phasor), vp, sz, sz, fp, sz, f, u64, sz, i, i, fp]),
         "or_rx_chain": (sz, [fp, sz, f, u64, i, fp, sz, sz, sz, P(Slicer), fp, vp, sz]),
+        "or_demodulate_front": (sz, [f, fp, sz, fp, sz, fp, sz, fp, fp, fp]),
         "or_modulate_cli": (c.c_long, [c.c_char_p, sz, sz, sz, sz, i, c.c_char_p, sz, fp, sz]),
     }
     for name, (res, args) in sig.items():
@@ -345,3 +346,16 @@ def ascii_reader(text: bytes, sps: int, bps: int) -> AsciiBits:
 def ascii_updates(text: bytes, sps: int, bps: int, n: int):
     a = ascii_reader(text, sps, bps)
     return _drain(lib().or_ascii_next, a, bps, n)
+
+
+def demodulate_front(sf: float, x: np.ndarray, hilbert: np.ndarray, lowpass: np.ndarray):
+    """or_demodulate_front: (i, q) per sample after the 64-sample PLL lock, and the offset."""
+    x = np.ascontiguousarray(x, np.float32)
+    h = np.ascontiguousarray(hilbert, np.float32)
+    lp = np.ascontiguousarray(lowpass, np.float32)
+    n = len(x)
+    oi = np.zeros(max(n - 64, 1), np.float32)
+    oq = np.zeros(max(n - 64, 1), np.float32)
+    off = np.zeros(1, np.float32)
+    k = lib().or_demodulate_front(sf, _fp(x), n, _fp(h), len(h), _fp(lp), len(lp), _fp(oi), _fp(oq), _fp(off))
+    return oi[:k], oq[:k], float(off[0])

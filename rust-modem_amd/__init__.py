@@ -102,7 +102,8 @@ class _RxDesc(ctypes.Structure):
                 ("taps", ctypes.POINTER(ctypes.c_float)), ("ntaps", ctypes.c_uint32),
                 ("decim", ctypes.c_uint32), ("decim_offset", ctypes.c_uint32),
                 ("mix", ctypes.c_int32), ("in_dtype", ctypes.c_int32),
-                ("out_dtype", ctypes.c_int32), ("slicer", _SlicerDesc)]
+                ("out_dtype", ctypes.c_int32), ("slicer", _SlicerDesc),
+                ("phase_offset", ctypes.c_float)]
 
 
 _lib = None
@@ -135,6 +136,7 @@ def load_library():
         "modem_abi_version": (c.c_int32, []),
         "modem_freq_sample_freq": (f32, [u64, u64]),
         "modem_rates_sps": (st, [u64, u64, c.POINTER(u64)]),
+        "modem_pll_lock": (st, [f32, u64, fp, sz, fp]),
         "modem_carrier_phase": (f32, [f32, u64]),
         "modem_carrier_phases": (st, [f32, u64, sz, vp, c.c_int, vp]),
         "modem_phasor_bits": (st, [c.POINTER(_PhasorDesc), c.POINTER(u32)]),
@@ -608,7 +610,8 @@ class DemodulatorRx:
 
     def __init__(self, carrier: Carrier, taps: np.ndarray, decim: int = 1, decim_offset: int = 0,
                  mix: int = MIX_REFERENCE_REAL, slicer: Optional[_SlicerDesc] = None,
-                 in_dtype: int = DTYPE_F32, out_dtype: int = DTYPE_F32, device: int = 0):
+                 in_dtype: int = DTYPE_F32, out_dtype: int = DTYPE_F32, device: int = 0,
+                 phase_offset: float = 0.0):
         L = load_library()
         self.carrier, self.decim, self.out_dtype, self.in_dtype = carrier, int(decim), out_dtype, in_dtype
         self.taps = np.ascontiguousarray(taps, dtype=np.float32)
@@ -620,6 +623,7 @@ class DemodulatorRx:
         d.ntaps = len(self.taps)
         d.decim, d.decim_offset, d.mix = self.decim, self.decim_offset, mix
         d.in_dtype, d.out_dtype = in_dtype, out_dtype
+        d.phase_offset = float(phase_offset)
         if slicer is not None:
             d.slicer = slicer
         else:
@@ -674,6 +678,45 @@ class DemodulatorRx:
 
 
 # --------------------------------------------------------------------- FIR (B5) ----
+LOCK_SAMPLES = 64   # demodulator.rs:5
+
+
+class Demodulator:
+    """Demodulator (demodulator.rs:7-56) with its PLL lock, as the `demodulate` binary drives it
+    (demodulate.rs:29-43): `lock_phase(sig)` runs PLL::handle (pll.rs:16-22) over the first 64
+    complex samples (host, modem_pll_lock: 64 serial steps of control logic), then `process`
+    gives (2*FIR(x.re*cos), 2*FIR(-x.re*sin)) at every further sample on the GPU with the locked
+    offset (`phase = carrier.next() + pll.phase_offset`, demodulator.rs:50).
+    `sig`: (n, 2) float32 (re, im) — a CUDA tensor or a numpy array."""
+
+    def __init__(self, carrier: Carrier, lowpass: np.ndarray, device: int = 0):
+        self.carrier, self.lowpass, self.device = carrier, np.ascontiguousarray(lowpass, np.float32), device
+        self.phase_offset = 0.0
+        self._rx = None
+
+    def lock_phase(self, sig):
+        """Consume the first 64 samples of `sig` (demodulator.rs:32-36); returns the rest."""
+        head = sig[:LOCK_SAMPLES]
+        if int(head.shape[0]) < LOCK_SAMPLES:
+            raise ModemPanic(ERR_INVALID_ARG, "lock_phase: called `Option::unwrap()` on a `None` value")
+        h = np.ascontiguousarray(head.detach().cpu().numpy() if _is_torch(head) else head, np.float32)
+        off = (ctypes.c_float * 1)(self.phase_offset)
+        _check(load_library().modem_pll_lock(self.carrier.sample_freq, self.carrier.sample, _fptr(h),
+                                             LOCK_SAMPLES, off), "Demodulator.lock_phase")
+        self.phase_offset = float(off[0])
+        self.carrier.sample += LOCK_SAMPLES
+        return sig[LOCK_SAMPLES:]
+
+    def process(self, sig, stream=None):
+        """(n, 2) float32 (i, q), one per input sample (Iterator::next, demodulator.rs:44-56)."""
+        if self._rx is None:
+            self._rx = DemodulatorRx(self.carrier, self.lowpass, decim=1, decim_offset=0,
+                                     mix=MIX_REFERENCE_REAL, device=self.device,
+                                     phase_offset=self.phase_offset)
+        iq, _ = self._rx.process(sig, want_sym=False, stream=stream)
+        return iq
+
+
 class FIRFilter:
     """FIRFilter (fir.rs:3-35): causal FIR, zero initial history, one output per input."""
 

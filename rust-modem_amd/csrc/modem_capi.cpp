@@ -211,6 +211,19 @@ float modem_freq_sample_freq(uint64_t hz, uint64_t sr) {           // freq.rs:19
     return ang / (float)sr;
 }
 
+modem_status modem_pll_lock(float w, uint64_t s0, const float* x, size_t n, float* off) {
+    if (!off || (n && !x)) return MODEM_ERR_INVALID_ARG;
+    const float change = 0.447214f;                                          // pll.rs:3
+    for (size_t k = 0; k < n; ++k) {                                         // demodulator.rs:33-35
+        const float inner = mod_trig(w * (float)(s0 + k)) + *off;            // pll.rs:17
+        const float cr = std::cos(inner), ci = -std::sin(inner);             // Complex::new(cos, sin).conj()
+        const float re = x[2 * k] * cr - x[2 * k + 1] * ci;                  // num::Complex Mul
+        const float im = x[2 * k] * ci + x[2 * k + 1] * cr;
+        *off += change * std::atan2(im, re);                                 // pll.rs:19-21
+    }
+    return MODEM_OK;
+}
+
 modem_status modem_rates_sps(uint64_t br, uint64_t sr, uint64_t* sps) {   // rates.rs:12-18
     if (!sps || br == 0) return MODEM_ERR_INVALID_ARG;
     *sps = sr / br;
@@ -625,6 +638,7 @@ struct modem_rx {
     int mix = 0, in_dtype = 0, out_dtype = 0;
     float w = 0.f;
     uint64_t c0 = 0;
+    float phase_offset = 0.f;       // PLL offset (demodulator.rs:50)
     int64_t consumed = 0;          // stream samples processed
     modem_slicer_desc slicer{};
     int mfma_ksteps = 0;            // > 0: matched filter on the matrix pipe (rx_mfma)
@@ -676,6 +690,7 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
     h->out_dtype = d->out_dtype;
     h->w = d->sample_freq;
     h->c0 = d->s0;
+    h->phase_offset = d->phase_offset;
     h->slicer = sl;
     h->slicer.lut = nullptr;
     // pp[b*K + t] = h[b + decim*t], padded for the kernels' look-ahead tap loads
@@ -795,6 +810,7 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
     p.D = (int)h->D;
     p.decim = (int)h->decim;
     p.x_aligned16 = ((uintptr_t)din % 16) == 0 ? 1 : 0;
+    p.phase_offset = h->phase_offset;
     p.small_n = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 32) ? 1 : 0;
     p.slicer_kind = h->slicer.kind;
     p.bps = (int)h->slicer.bits_per_symbol;

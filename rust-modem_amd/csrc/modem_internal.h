@@ -90,6 +90,7 @@ struct RxParams {
     float max_symbol;
     float w;
     int32_t tap_scale_exp;   // rx_mfma: tables hold h * 2^tap_scale_exp
+    float phase_offset;      // PLL offset added to the carrier phase (demodulator.rs:50)
 };
 
 struct FirParams {

@@ -78,13 +78,19 @@ __device__ __forceinline__ void rx_pair(const RxParams& p, int64_t q, float2& a,
     }
 }
 
+// carrier.next() + pll.phase_offset (demodulator.rs:50): one f32 add, exact for offset 0
+__device__ __forceinline__ float rx_phase(const RxParams& p, float carrier) {
+#pragma clang fp contract(off)
+    return carrier + p.phase_offset;
+}
+
 // x * e^{-j phase} (or the reference's x.re * (cos, -sin), demodulator.rs:46,53-54) for
 // stream index n = nb + off (nb wave-uniform).
 template <int MIX>
 __device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t nb, int off, float2 x) {
     if (nb + off < 0) return make_float2(0.f, 0.f);   // before the stream: zero history
     float s, c;
-    sincos_phase(carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.small_n), s, c);
+    sincos_phase(rx_phase(p, carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.small_n)), s, c);
     if (MIX == MIX_REFERENCE_REAL) return make_float2(x.x * c, x.x * -s);
     return make_float2(__builtin_fmaf(x.y, s, x.x * c), __builtin_fmaf(-x.x, s, x.y * c));
 }
@@ -187,7 +193,7 @@ __device__ __forceinline__ void rx_stage_fast(const RxParams& p, float2* lds, in
 #ifdef MODEM_ABLATE_MIX
                 s = 0.f; c = (float)(nb32 + (uint32_t)e);
 #else
-                sincos_phase(phase_from_f(p.w, (float)(nb32 + (uint32_t)e)), s, c);
+                sincos_phase(rx_phase(p, phase_from_f(p.w, (float)(nb32 + (uint32_t)e))), s, c);
 #endif
                 float2 z;
                 if (MIX == MIX_REFERENCE_REAL) z = make_float2(x[j].x * c, x[j].x * -s);
@@ -517,7 +523,7 @@ struct RxMfma {
 #ifdef MODEM_ABLATE_MIX
                 sn = 0.f; cs = __uint_as_float(0x3f000000u | ((lb + (uint32_t)(4 * NT * u + j)) & 0xffu));
 #else
-                sincos_phase(phase_from_f(p.w, (float)(lb + (uint32_t)(4 * NT * u + j))), sn, cs);
+                sincos_phase(rx_phase(p, phase_from_f(p.w, (float)(lb + (uint32_t)(4 * NT * u + j)))), sn, cs);
 #endif
                 if (MIX == MIX_REFERENCE_REAL) { zr[j] = x[j].x * cs; zi[j] = x[j].x * -sn; }
                 else {
