@@ -578,7 +578,7 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     p.K = (int)h->K;
     p.fast_bits = (h->ncarry == 0 && (h->bps == 1 || h->bps == 2 || h->bps == 4 || h->bps == 8) &&
                    ((uintptr_t)dbits % h->bps) == 0) ? 1 : 0;
-    p.small_n = (h->sample + nsamp) <= (1ull << 32) ? 1 : 0;
+    p.exact_idx = (h->sample + nsamp) <= (1ull << 53) ? 1 : 0;
     p.w = h->w;
     p.lut_h = h->d_luth;
     p.lut_scale_exp = h->lut_scale_exp;
@@ -811,7 +811,7 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
     p.decim = (int)h->decim;
     p.x_aligned16 = ((uintptr_t)din % 16) == 0 ? 1 : 0;
     p.phase_offset = h->phase_offset;
-    p.small_n = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 32) ? 1 : 0;
+    p.exact_idx = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 53) ? 1 : 0;
     p.slicer_kind = h->slicer.kind;
     p.bps = (int)h->slicer.bits_per_symbol;
     p.bits_per_carrier = (int)h->slicer.bits_per_carrier;

@@ -35,16 +35,24 @@ __device__ __forceinline__ float phase_from_f(float w, float nf) {
     return x - p;
 }
 
-// `n as f32` with round-to-nearest-even: one v_cvt_f32_u32 below 2^32, the compiler's
-// exact u64 -> f32 sequence above.
-__device__ __forceinline__ float carrier_phase(float w, uint64_t n, bool small_n) {
-    const float nf = small_n ? (float)(uint32_t)n : (float)n;
+// `n as f32` with round-to-nearest-even. Below 2^53 (`exact_idx`, checked on the host per
+// call) the index is exact as an f64 and one v_cvt_f32_f64 rounds it once, as rustc's u64 -> f32
+// does; the hot loops keep a per-lane f64 index and add the per-sample offset in f64 (no
+// 32-bit index wrap at 2^32, so streams longer than 4.3 Gsamples stay on the fast paths).
+// At and above 2^53 the compiler's exact u64 -> f32 sequence.
+__device__ __forceinline__ float idx_f32(double nd) { return (float)nd; }
+
+__device__ __forceinline__ float carrier_phase(float w, uint64_t n, bool exact_idx) {
+    const float nf = exact_idx ? idx_f32((double)n) : (float)n;
     return phase_from_f(w, nf);
 }
 
-// Same, for n = base + off with a wave-uniform 64-bit base and a 32-bit lane offset.
-__device__ __forceinline__ float carrier_phase_off(float w, uint64_t base, int off, bool small_n) {
-    const float nf = small_n ? (float)((uint32_t)base + (uint32_t)off) : (float)(base + (int64_t)off);
+// Same, for n = base + off with a wave-uniform 64-bit base and a 32-bit lane offset. The add is
+// done in u64 first: callers may pass a base "before the stream" (wrapped below 0) with an
+// offset that brings n back to >= 0, which an f64 add of the two parts would not reproduce.
+__device__ __forceinline__ float carrier_phase_off(float w, uint64_t base, int off, bool exact_idx) {
+    const uint64_t n = base + (uint64_t)(int64_t)off;
+    const float nf = exact_idx ? idx_f32((double)n) : (float)n;
     return phase_from_f(w, nf);
 }
 

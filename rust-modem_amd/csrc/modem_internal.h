@@ -29,7 +29,7 @@ struct TxParams {
     int32_t sps;             // runtime samples/symbol (generic kernel)
     int32_t K;               // taps per polyphase branch = ceil(ntaps / sps)
     int32_t fast_bits;       // ncarry == 0, bps in {1,2,4,8}, bits aligned to bps bytes
-    int32_t small_n;         // every carrier index of this call is < 2^32
+    int32_t exact_idx;       // every carrier index of this call is < 2^53 (exact as f64)
     float w;                 // Freq::sample_freq()
     // tx_mfma (split-f16 FIR): LUT as (re_hi, re_lo, im_hi, im_lo) halves of lut * 2^lut_scale_exp,
     // B fragments hold taps * 2^tap_scale_exp; lead = symbols before this call, mod 16/sps.
@@ -82,7 +82,7 @@ struct RxParams {
     int32_t D;               // decim_offset
     int32_t decim;           // runtime decimation (generic kernel)
     int32_t x_aligned16;     // x is 16-byte aligned (pair loads)
-    int32_t small_n;
+    int32_t exact_idx;
     int32_t slicer_kind;
     int32_t bps;
     int32_t bits_per_carrier;

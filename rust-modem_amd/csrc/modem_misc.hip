@@ -60,17 +60,17 @@ __global__ __launch_bounds__(256) void fir_real(const FirParams p) {
 }
 
 // ----------------------------------------------------------- carrier phases (tests) ----
-__global__ __launch_bounds__(256) void carrier_phases(float w, uint64_t s0, size_t n, int small_n,
+__global__ __launch_bounds__(256) void carrier_phases(float w, uint64_t s0, size_t n, int exact_idx,
                                                       float* out) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = carrier_phase(w, s0 + i, small_n != 0);
+    if (i < n) out[i] = carrier_phase(w, s0 + i, exact_idx != 0);
 }
 
 hipError_t launch_phases(float w, uint64_t s0, size_t n, float* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const int small_n = (s0 + n) <= (1ull << 32) ? 1 : 0;
+    const int exact_idx = (s0 + n) <= (1ull << 53) ? 1 : 0;
     hipLaunchKernelGGL(carrier_phases, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, s0, n,
-                       small_n, out);
+                       exact_idx, out);
     return hipGetLastError();
 }
 

@@ -90,7 +90,7 @@ template <int MIX>
 __device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t nb, int off, float2 x) {
     if (nb + off < 0) return make_float2(0.f, 0.f);   // before the stream: zero history
     float s, c;
-    sincos_phase(rx_phase(p, carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.small_n)), s, c);
+    sincos_phase(rx_phase(p, carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.exact_idx)), s, c);
     if (MIX == MIX_REFERENCE_REAL) return make_float2(x.x * c, x.x * -s);
     return make_float2(__builtin_fmaf(x.y, s, x.x * c), __builtin_fmaf(-x.x, s, x.y * c));
 }
@@ -158,7 +158,7 @@ __device__ __forceinline__ void rx_mac(cf2 (&acc)[R], const cf2 (&win)[R], float
 // per-plane base); lanes read with stride R (odd) -> conflict-free ds_read_b64.
 __host__ __device__ inline int rx_plane_stride(int TS, int K) { return (TS + K) | 1; }
 
-// Rare path (first / last tile of a chunk, unaligned input, carrier index >= 2^32): one
+// Rare path (first / last tile of a chunk, unaligned input, carrier index >= 2^53): one
 // sample at a time with full 64-bit bookkeeping, as one rolled loop under a uniform branch
 // (never called out of line: a call would push the kernel arguments to per-lane scratch).
 template <int DEC, typename InT, int MIX>
@@ -172,14 +172,18 @@ __device__ __forceinline__ void rx_stage_slow(const RxParams& p, float2* lds, in
     }
 }
 
-// Steady state: every staged sample lies inside the chunk and below carrier index 2^32.
+// Steady state: every staged sample lies inside the chunk and below carrier index 2^53.
 // Slot u of lane tid holds samples e = 2*(tid + NT*u) - PAR + {0,1}; the per-slot part of
 // every index is a compile-time constant (NT*2/DEC plane elements per slot), so the LDS
-// stores use immediate offsets and the phase needs one 32-bit add.
+// stores use immediate offsets and the phase needs one f64 add.
 template <int DEC, typename InT, int MIX, int PAR, int U, int NT>
 __device__ __forceinline__ void rx_stage_fast(const RxParams& p, float2* lds, int PS, int NS,
-                                              uint32_t nb32, const typename InIO<InT>::Raw (&pre)[U]) {
+                                              double nbd, const typename InIO<InT>::Raw (&pre)[U]) {
     const int tid = threadIdx.x;
+    // carrier index of the lane's first sample; opaque, so that the per-sample offsets stay
+    // f64 literals instead of hoisted VGPR pairs
+    double lb = nbd + (double)(2 * tid - PAR);
+    asm volatile("" : "+v"(lb));
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         float2 x[2];
@@ -191,9 +195,9 @@ __device__ __forceinline__ void rx_stage_fast(const RxParams& p, float2* lds, in
             if (e >= 0 && e < NS) {
                 float s, c;
 #ifdef MODEM_ABLATE_MIX
-                s = 0.f; c = (float)(nb32 + (uint32_t)e);
+                s = 0.f; c = idx_f32(lb + (double)(j + 2 * NT * u));
 #else
-                sincos_phase(rx_phase(p, phase_from_f(p.w, (float)(nb32 + (uint32_t)e))), s, c);
+                sincos_phase(rx_phase(p, phase_from_f(p.w, idx_f32(lb + (double)(j + 2 * NT * u)))), s, c);
 #endif
                 float2 z;
                 if (MIX == MIX_REFERENCE_REAL) z = make_float2(x[j].x * c, x[j].x * -s);
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
         return (p.k_first + t * TS) * DEC + p.D - (int64_t)K * DEC + 1 - p.n_start;
     };
     // A tile is "inside" when its prefetched slots are whole pairs of this chunk.
-    const bool pf = p.x_aligned16 && p.small_n && NS + 1 <= 2 * NT * U;   // workgroup-uniform
+    const bool pf = p.x_aligned16 && p.exact_idx && NS + 1 <= 2 * NT * U;   // workgroup-uniform
     auto inside = [&](int64_t q_lo) {
         const int64_t qb = q_lo - (q_lo & 1);
         return pf && qb >= 0 && qb + 2 * NT * U <= p.N;
@@ -247,9 +251,9 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
         const int64_t q_lo = q_lo_of(t);
         // 1. mix the tile's samples into DEC polyphase planes.
         if (inside(q_lo)) {
-            const uint32_t nb32 = (uint32_t)(p.c0 + (uint64_t)(q_lo - (q_lo & 1) + p.n_start));
-            if (q_lo & 1) rx_stage_fast<DEC, InT, MIX, 1, U, NT>(p, lds, PS, NS, nb32 + 1u, pre);
-            else rx_stage_fast<DEC, InT, MIX, 0, U, NT>(p, lds, PS, NS, nb32, pre);
+            const double nbd = (double)(p.c0 + (uint64_t)(q_lo - (q_lo & 1) + p.n_start));
+            if (q_lo & 1) rx_stage_fast<DEC, InT, MIX, 1, U, NT>(p, lds, PS, NS, nbd + 1.0, pre);
+            else rx_stage_fast<DEC, InT, MIX, 0, U, NT>(p, lds, PS, NS, nbd, pre);
         } else {
             rx_stage_slow<DEC, InT, MIX>(p, lds, PS, NS, q_lo);
         }
@@ -477,7 +481,7 @@ struct RxMfma {
         *reinterpret_cast<h4*>(pl + 3 * PL + o) = (h4){il0.x, il0.y, il1.x, il1.y};
     }
 
-    // Steady state: the tile's samples lie inside the chunk, carrier index < 2^32. Staged
+    // Steady state: the tile's samples lie inside the chunk, carrier index < 2^53. Staged
     // at scale 1 (the tile max is tracked on the way). Returns the tile's scale exponent: 0,
     // or for a tile whose max falls outside [2^-3, 2^15) the exponent the general path
     // (stage_slow) must restage it with.
@@ -499,12 +503,12 @@ struct RxMfma {
     // Steady-state staging of one tile from the prefetched registers `pre`. (Reloading each
     // slot for the next tile right after it is consumed, to give the loads a whole tile period,
     // measured 1 us slower on C3 than prefetching after the stage.)
-    __device__ static int stage_fast(const RxParams& p, _Float16* pl, float* red, uint32_t nb32,
+    __device__ static int stage_fast(const RxParams& p, _Float16* pl, float* red, double nbd,
                                      const QT (&pre)[U]) {
         const int tid = threadIdx.x;
         // carrier index of the lane's first sample; opaque, so that the per-sample offsets
         // stay immediates instead of 4*U hoisted loop-invariant VGPRs
-        uint32_t lb = nb32 + 4u * (uint32_t)tid;
+        double lb = nbd + (double)(4 * tid);
         int pos0 = ppos(4 * tid);                         // slot u writes at pos0 + u * SLOT_POS
         asm volatile("" : "+v"(lb), "+v"(pos0));
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -521,9 +525,9 @@ struct RxMfma {
             for (int j = 0; j < 4; ++j) {
                 float sn, cs;
 #ifdef MODEM_ABLATE_MIX
-                sn = 0.f; cs = __uint_as_float(0x3f000000u | ((lb + (uint32_t)(4 * NT * u + j)) & 0xffu));
+                sn = 0.f; cs = idx_f32(lb + (double)(4 * NT * u + j));
 #else
-                sincos_phase(rx_phase(p, phase_from_f(p.w, (float)(lb + (uint32_t)(4 * NT * u + j)))), sn, cs);
+                sincos_phase(rx_phase(p, phase_from_f(p.w, idx_f32(lb + (double)(4 * NT * u + j)))), sn, cs);
 #endif
                 if (MIX == MIX_REFERENCE_REAL) { zr[j] = x[j].x * cs; zi[j] = x[j].x * -sn; }
                 else {
@@ -550,7 +554,7 @@ struct RxMfma {
         return tile_scale_exp<NT>(mx, red);
     }
 
-    // First / last tiles of a chunk, unaligned input, carrier index >= 2^32: per sample, two
+    // First / last tiles of a chunk, unaligned input, carrier index >= 2^53: per sample, two
     // passes (max, then scale + split).
     __device__ static int stage_slow(const RxParams& p, _Float16* pl, float* red, int64_t q_lo) {
         const int64_t n_lo = q_lo + p.n_start;
@@ -664,7 +668,7 @@ struct RxMfma {
     // Tiles of [t0, t1) (a contiguous range per workgroup: measured 9 % faster on C3 than
     // handing neighbouring tiles to concurrently running workgroups, and dynamic tile handout
     // through per-XCD atomic counters did not beat it either). When the input is 8-B aligned
-    // and the carrier indices stay below 2^32, the run of "full" tiles (all staged samples
+    // and the carrier indices stay below 2^53, the run of "full" tiles (all staged samples
     // inside the chunk, all 1024 instants kept) goes through the prefetched loop, whose
     // epilogue EM stores unconditionally; the first and last tiles of the chunk take the
     // general path.
@@ -673,7 +677,7 @@ struct RxMfma {
                                int64_t t0, int64_t t1) {
         const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar
         // quad loads need dword alignment only (16-B loads at 8-B aligned sample offsets)
-        const bool fast = p.small_n && ((uintptr_t)p.x & 3) == 0;
+        const bool fast = p.exact_idx && ((uintptr_t)p.x & 3) == 0;
         const int kb = p.tap_scale_exp;
         const int ld = lead(p);
         auto full = [&](int64_t t) {
@@ -709,7 +713,7 @@ struct RxMfma {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     STAMP(1);                              // waiting for the tile's samples
 #endif
-                    const int ka = stage_fast(p, pl, red, (uint32_t)(p.c0 + (uint64_t)n_lo), pre);
+                    const int ka = stage_fast(p, pl, red, (double)(p.c0 + (uint64_t)n_lo), pre);
                     STAMP(2);                              // staging + tile-max barrier
                     if (ka != 0) { restage = true; break; }       // uniform; leaves the loop
                     // (the tile-max reduction in stage_fast ended with a barrier: planes visible)

@@ -68,10 +68,10 @@ __device__ void tx_state_update(const TxParams& p) {
 
 // Mix one filtered baseband sample onto the carrier (IQSample::modulate, modulator.rs:45-48).
 template <int OUT_MODE>
-__device__ __forceinline__ float2 tx_mix(float w, uint64_t n, bool small_n, float2 y) {
+__device__ __forceinline__ float2 tx_mix(float w, uint64_t n, bool exact_idx, float2 y) {
     if (OUT_MODE == OUT_IQ_BASEBAND) return y;
     float s, c;
-    sincos_phase(carrier_phase(w, n, small_n), s, c);
+    sincos_phase(carrier_phase(w, n, exact_idx), s, c);
     return make_float2(y.x * c - y.y * s, y.x * s + y.y * c);
 }
 
@@ -79,9 +79,9 @@ template <int OUT_MODE, typename OutT>
 __device__ __forceinline__ void tx_emit(const TxParams& p, int64_t j, float2 y0, float2 y1,
                                         bool two) {
     const uint64_t n = p.s0 + (uint64_t)j;
-    const float2 z0 = tx_mix<OUT_MODE>(p.w, n, p.small_n, y0);
+    const float2 z0 = tx_mix<OUT_MODE>(p.w, n, p.exact_idx, y0);
     if (two) {
-        const float2 z1 = tx_mix<OUT_MODE>(p.w, n + 1, p.small_n, y1);
+        const float2 z1 = tx_mix<OUT_MODE>(p.w, n + 1, p.exact_idx, y1);
         if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_pair(p.out, j, z0.x, z1.x);
         else OutIO<OutT>::store_pair(p.out, j, z0.x, z0.y, z1.x, z1.y);
     } else {
@@ -103,10 +103,10 @@ __device__ __forceinline__ void tx_emit_off(const TxParams& p, int64_t jb, int o
 #endif
         const uint64_t nb = p.s0 + (uint64_t)jb;
         float s, c;
-        sincos_phase(carrier_phase_off(p.w, nb, off, p.small_n), s, c);
+        sincos_phase(carrier_phase_off(p.w, nb, off, p.exact_idx), s, c);
         z0 = make_float2(y0.x * c - y0.y * s, y0.x * s + y0.y * c);
         if (two) {
-            sincos_phase(carrier_phase_off(p.w, nb, off + 1, p.small_n), s, c);
+            sincos_phase(carrier_phase_off(p.w, nb, off + 1, p.exact_idx), s, c);
             z1 = make_float2(y1.x * c - y1.y * s, y1.x * s + y1.y * c);
         }
     }
@@ -406,14 +406,14 @@ struct TxMfma {
         dim = m0;
     }
 
-    // Full 16x16 tile, carrier index < 2^32: unconditional stores. jt = call sample index of
+    // Full 16x16 tile, carrier index < 2^53: unconditional stores. jt = call sample index of
     // the sub-tile's first sample. Per sample: packed unscale (2^-kab), bit-exact phase,
     // sin/cos, packed mix; stores through a uniform base + 32-bit lane offsets.
     __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
         const int lane = threadIdx.x & 63;
         int loff = 64 * (lane >> 4) + (lane & 15);          // sample of row r: loff + 16 r
         asm volatile("" : "+v"(loff));
-        const uint32_t nb = (uint32_t)(p.s0 + (uint64_t)jt) + (uint32_t)loff;
+        const double nb = (double)(p.s0 + (uint64_t)jt) + (double)loff;
         cf2 z[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) z[r] = (cf2){dre[r], dim[r]};
@@ -426,7 +426,7 @@ struct TxMfma {
 #ifndef MODEM_ABLATE_MIX
             if (OUT_MODE != OUT_IQ_BASEBAND) {
                 float sn, cs;
-                sincos_phase(phase_from_f(p.w, (float)(nb + (uint32_t)(16 * r))), sn, cs);
+                sincos_phase(phase_from_f(p.w, idx_f32(nb + (double)(16 * r))), sn, cs);
                 z[r] = tx_cmix(z[r], (cf2){cs, sn});
             }
 #endif
@@ -449,7 +449,7 @@ struct TxMfma {
 #endif
     }
 
-    // Partial tile, samples before the call, or carrier index >= 2^32: guarded, 64-bit
+    // Partial tile, samples before the call, or carrier index >= 2^53: guarded, 64-bit
     // indices; the same arithmetic as emit_full (a sample's bits never depend on the path).
     __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
         const int lane = threadIdx.x & 63;
@@ -461,7 +461,7 @@ struct TxMfma {
             cf2 z = (cf2){dre[r], dim[r]} * unscale;
             if (OUT_MODE != OUT_IQ_BASEBAND) {
                 float sn, cs;
-                sincos_phase(carrier_phase_off(p.w, p.s0 + (uint64_t)jt, off, p.small_n), sn, cs);
+                sincos_phase(carrier_phase_off(p.w, p.s0 + (uint64_t)jt, off, p.exact_idx), sn, cs);
                 z = tx_cmix(z, (cf2){cs, sn});
             }
             if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, jt + off, z.x);
@@ -470,7 +470,7 @@ struct TxMfma {
     }
 
     // Tiles t0, t0 + ts, ... below t1. Tile t holds symbols [t*TS - lead, (t+1)*TS - lead) of the call. BPS > 0: bits aligned,
-    // no leftover bits, carrier index < 2^32 (the steady state); BPS == 0: general path only.
+    // no leftover bits, carrier index < 2^53 (the steady state); BPS == 0: general path only.
     template <int BPS>
     __device__ static void run(const TxParams& p, _Float16* pl, const th4* lut_s, const th8 (&bh)[NKS],
                                const th8 (&bl)[NKS], int64_t t0, int64_t t1, int64_t ts) {
@@ -558,7 +558,7 @@ __global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __re
     // tiles (measured 1 % faster on C3 than contiguous ranges per workgroup)
     const int64_t t0 = blockIdx.x, t1 = ntiles, ts = gridDim.x;
     if (t0 >= t1) return;
-    if (p.fast_bits && p.small_n) {              // one uniform switch: the tile loop is specialised
+    if (p.fast_bits && p.exact_idx) {              // one uniform switch: the tile loop is specialised
         switch (p.bps) {
         case 1: K::template run<1>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
         case 2: K::template run<2>(p, pl, lut_s, bh, bl, t0, t1, ts); return;

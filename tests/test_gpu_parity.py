@@ -254,6 +254,30 @@ def test_rx_other_rates(m, o, torch_cuda, decim, L, fir_path):
     assert np.array_equal(host(gsym), rsym)
 
 
+@pytest.mark.parametrize("s0", [2**32 - 5000, 2**40 + 3, 2**53 - 6000])
+def test_long_stream_carrier_index(m, o, torch_cuda, s0, fir_path):
+    """Carrier indices past 2^32 (a stream older than 4.3 Gsamples) take the same fast kernels
+    (the index is kept in f64, exact below 2^53); a call that reaches 2^53 takes the general
+    path's u64 -> f32 conversion. TX and RX against the oracle started at the same index."""
+    name, bps, L, sps = CONFIGS["c3_qam16"]
+    nsym = 3000
+    bits = o.prng_bits(SEED + 13, nsym * bps)
+    taps = m.rrc_taps(L, sps, 0.35)
+    w = w_quarter(o)
+    flush = (L - 1 + sps - 1) // sps
+    y = gpu_tx(m, torch_cuda, name, bits, sps, taps, w, s0=s0, flush=True)
+    x = o.tx_chain(oracle_phasor(o, name), bits, sps, taps, w, s0, flush_syms=flush)
+    assert y.shape[0] == x.shape[0]
+    assert np.abs(host(y) - x).max() <= tol_for(L) * np.abs(x).max()
+    riq, rsym = o.rx_chain(x, w, s0, o.MIX_COMPLEX, taps, sps, L - 1, oracle_slicer(o, name, bps))
+    rx = m.DemodulatorRx(m.Carrier(w, s0), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                         slicer=product_phasor(m, name).slicer())
+    giq, gsym = rx.process(torch_cuda.from_numpy(x).cuda())
+    assert np.abs(host(giq) - riq).max() <= tol_for(L) * np.abs(riq).max()
+    assert np.array_equal(host(gsym), rsym)
+    assert np.array_equal(host(gsym)[:nsym], sent_symbols(bits, bps))
+
+
 # ------------------------------------------------------------------- FIRFilter ----
 @pytest.mark.parametrize("L", [1, 2, 23, 64, 129, 1000])
 def test_fir_filter(m, o, torch_cuda, L):
