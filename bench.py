@@ -107,32 +107,37 @@ class GpuRunner:
     def sync(self):
         self.torch.cuda.synchronize()
 
-    def kernel_times_ms(self, reps):
+    def kernel_times_ms(self, reps, rounds=5):
         """Mean device time of the TX and RX launches, from HIP events on the launch stream.
 
         Events between every pair of kernels add their own gaps, so the chain is timed as
         `reps` back-to-back TX+RX steps between two events, TX alone as `reps` back-to-back TX
         launches, and RX as the difference. Untimed steps are queued first so that the device
-        has a backlog (events recorded while it waits for the host would time the host)."""
+        has a backlog (events recorded while it waits for the host would time the host). The
+        pair is measured `rounds` times, interleaved, and the medians are reported (a single
+        round swings by a few us with the clocks)."""
         torch = self.torch
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        for _ in range(16):
-            self.tx(0)
-            self.rx(0)
-        ev[0].record(self.stream)
-        for _ in range(reps):
-            self.tx(0)
-            self.rx(0)
-        ev[1].record(self.stream)
-        for _ in range(8):
-            self.tx(0)
-        ev[2].record(self.stream)
-        for _ in range(reps):
-            self.tx(0)
-        ev[3].record(self.stream)
-        torch.cuda.synchronize()
-        t_chain = ev[0].elapsed_time(ev[1]) / reps
-        t_tx = ev[2].elapsed_time(ev[3]) / reps
+        chain, tx = [], []
+        for _ in range(rounds):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            for _ in range(16):
+                self.tx(0)
+                self.rx(0)
+            ev[0].record(self.stream)
+            for _ in range(reps):
+                self.tx(0)
+                self.rx(0)
+            ev[1].record(self.stream)
+            for _ in range(8):
+                self.tx(0)
+            ev[2].record(self.stream)
+            for _ in range(reps):
+                self.tx(0)
+            ev[3].record(self.stream)
+            torch.cuda.synchronize()
+            chain.append(ev[0].elapsed_time(ev[1]) / reps)
+            tx.append(ev[2].elapsed_time(ev[3]) / reps)
+        t_chain, t_tx = sorted(chain)[rounds // 2], sorted(tx)[rounds // 2]
         return t_tx, t_chain - t_tx
 
     def check(self):

@@ -35,6 +35,23 @@ __device__ __forceinline__ float phase_from_f(float w, float nf) {
     return x - p;
 }
 
+// (re, im) pair: one v_pk_fma_f32 per complex x real MAC, tap broadcast from an SGPR.
+typedef float cf2 __attribute__((ext_vector_type(2)));
+
+// phase_from_f for two indices at once on the packed f32 VALU (v_pk_mul/v_pk_fma/v_pk_add_f32
+// round each half exactly as the scalar ops do, so both phases are bit-identical to
+// phase_from_f; two samples per issue, floor stays scalar).
+__device__ __forceinline__ cf2 phase_from_f2(float w, cf2 nf) {
+#pragma clang fp contract(off)
+    const cf2 x = nf * w;
+    const cf2 q0 = x * kRcp2Pi;
+    const cf2 r = __builtin_elementwise_fma(-q0, (cf2){kTwoPi, kTwoPi}, x);
+    const cf2 q1 = __builtin_elementwise_fma(r, (cf2){kRcp2Pi, kRcp2Pi}, q0);
+    const cf2 f = (cf2){__builtin_floorf(q1.x), __builtin_floorf(q1.y)};
+    const cf2 p = f * kTwoPi;
+    return x - p;
+}
+
 // `n as f32` with round-to-nearest-even. Below 2^53 (`exact_idx`, checked on the host per
 // call) the index is exact as an f64 and one v_cvt_f32_f64 rounds it once, as rustc's u64 -> f32
 // does; the hot loops keep a per-lane f64 index and add the per-sample offset in f64 (no
@@ -85,9 +102,20 @@ __device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
 #endif
 }
 
+// Hardware sin/cos of two phases (what __sinf/__cosf compile to: v_sin/v_cos of phase/2pi,
+// here with one packed multiply for both samples).
+__device__ __forceinline__ void sincos_phase2(cf2 ph, cf2& s, cf2& c) {
+#if defined(MODEM_ABLATE_TRIG) || defined(MODEM_PRECISE_TRIG)
+    sincos_phase(ph.x, s.x, c.x);
+    sincos_phase(ph.y, s.y, c.y);
+#else
+    const cf2 rev = ph * kRcp2Pi;
+    s = (cf2){__builtin_amdgcn_sinf(rev.x), __builtin_amdgcn_sinf(rev.y)};
+    c = (cf2){__builtin_amdgcn_cosf(rev.x), __builtin_amdgcn_cosf(rev.y)};
+#endif
+}
+
 typedef const __attribute__((address_space(4))) float cfloat;   // wave-uniform -> s_load
-// (re, im) pair: one v_pk_fma_f32 per complex x real MAC, tap broadcast from an SGPR.
-typedef float cf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ cf2 ldc(const float2* p) { return *reinterpret_cast<const cf2*>(p); }
 __device__ __forceinline__ cf2 cmac(cf2 x, float h, cf2 acc) {
     return __builtin_elementwise_fma(x, (cf2){h, h}, acc);

@@ -360,15 +360,20 @@ __device__ __forceinline__ void split2(cf2 v, h2& hi, h2& lo) {
 }
 
 // Conjugate mix of one sample, packed: (re, im) = (x*cs + y*sn, y*cs - x*sn) with the same
-// roundings as fma(y, sn, x*cs) / fma(-x, sn, y*cs). cssn = (cs, sn), typically straight from
-// v_sin/v_cos: gfx950 needs one wait state before a VALU reads a transcendental's result, and
-// the compiler's hazard recognizer does not look inside inline asm, hence the s_nop.
+// roundings as fma(y, sn, x*cs) / fma(-x, sn, y*cs). cssn = (cs, sn). Written as vector ops
+// (v_pk_mul_f32 + v_pk_fma_f32 with op_sel / neg modifiers), so that the compiler's hazard
+// recognizer sees them and only pads where a transcendental's result is read too early.
 __device__ __forceinline__ cf2 cmix(cf2 x, cf2 cssn) {
+#ifdef MODEM_CMIX_ASM
     cf2 t, z;
     asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(x), "v"(cssn));
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
         : "=v"(z) : "v"(x), "v"(cssn), "v"(t));
     return z;
+#else
+    const cf2 t = x * cssn.xx;
+    return __builtin_elementwise_fma((cf2){x.y, -x.x}, cssn.yy, t);
+#endif
 }
 
 // Four consecutive input samples (one lane's staging quad).
@@ -521,22 +526,36 @@ struct RxMfma {
             Q::split(pre[u], x);
             const int e0 = 4 * (tid + NT * u);
             float zr[4], zi[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float sn, cs;
+            // the quad's phases as two packed pairs, computed side by side (independent
+            // chains fill each other's VALU dependency wait states)
+            cf2 sn2[2], cs2[2];
+            {
+                const cf2 nf0 = (cf2){idx_f32(lb + (double)(4 * NT * u)), idx_f32(lb + (double)(4 * NT * u + 1))};
+                const cf2 nf1 = (cf2){idx_f32(lb + (double)(4 * NT * u + 2)), idx_f32(lb + (double)(4 * NT * u + 3))};
 #ifdef MODEM_ABLATE_MIX
-                sn = 0.f; cs = idx_f32(lb + (double)(4 * NT * u + j));
+                sn2[0] = sn2[1] = (cf2){0.f, 0.f}; cs2[0] = nf0; cs2[1] = nf1;
 #else
-                sincos_phase(rx_phase(p, phase_from_f(p.w, idx_f32(lb + (double)(4 * NT * u + j)))), sn, cs);
+                // rx_phase: one add on the packed phases (no product to contract)
+                const cf2 ph0 = phase_from_f2(p.w, nf0) + p.phase_offset;
+                const cf2 ph1 = phase_from_f2(p.w, nf1) + p.phase_offset;
+                sincos_phase2(ph0, sn2[0], cs2[0]);
+                sincos_phase2(ph1, sn2[1], cs2[1]);
 #endif
-                if (MIX == MIX_REFERENCE_REAL) { zr[j] = x[j].x * cs; zi[j] = x[j].x * -sn; }
-                else {
-                    const cf2 z = cmix((cf2){x[j].x, x[j].y}, (cf2){cs, sn});
-                    zr[j] = z.x; zi[j] = z.y;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j += 2) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const float sn = sn2[j / 2][i], cs = cs2[j / 2][i];
+                    if (MIX == MIX_REFERENCE_REAL) { zr[j + i] = x[j + i].x * cs; zi[j + i] = x[j + i].x * -sn; }
+                    else {
+                        const cf2 z = cmix((cf2){x[j + i].x, x[j + i].y}, (cf2){cs, sn});
+                        zr[j + i] = z.x; zi[j + i] = z.y;
+                    }
+                    // only the last slot can reach past the tile: its extra samples are not counted
+                    if ((u + 1) * 4 * NT <= NS || e0 + j + i < NS)      // one v_max3 per sample
+                        asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j + i]), "v"(zi[j + i]));
                 }
-                // only the last slot can reach past the tile: its extra samples are not counted
-                if ((u + 1) * 4 * NT <= NS || e0 + j < NS)      // one v_max3 per sample
-                    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j]), "v"(zi[j]));
             }
 #ifdef MODEM_ABLATE_PUT
             asm volatile("" :: "v"(zr[0]), "v"(zr[1]), "v"(zr[2]), "v"(zr[3]), "v"(zi[0]), "v"(zi[1]), "v"(zi[2]), "v"(zi[3]));

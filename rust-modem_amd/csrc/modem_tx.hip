@@ -289,11 +289,18 @@ template <int SPS> struct TxMfmaCfg {
 // Carrier mix of one sample, packed: (re, im) = (y*cs - yi*sn, y*sn + yi*cs), y = (yr, yi),
 // cssn = (cs, sn) straight from v_sin/v_cos (hence the wait state, see cmix in modem_rx.hip).
 __device__ __forceinline__ cf2 tx_cmix(cf2 y, cf2 cssn) {
+#ifdef MODEM_CMIX_ASM
     cf2 t, z;
     asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(y), "v"(cssn));
     asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]"
         : "=v"(z) : "v"(y), "v"(cssn), "v"(t));
     return z;
+#else
+    // vector ops (v_pk_mul_f32 + v_pk_fma_f32 with op_sel / neg modifiers): visible to the
+    // compiler's hazard recognizer, which pads only where a v_sin/v_cos result is read too early
+    const cf2 t = y * cssn.xx;
+    return __builtin_elementwise_fma(y.yx, (cf2){-cssn.y, cssn.y}, t);
+#endif
 }
 
 typedef _Float16 th8 __attribute__((ext_vector_type(8)));
@@ -421,16 +428,21 @@ struct TxMfma {
 #pragma unroll
             for (int r = 0; r < 4; ++r) z[r] *= unscale;
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
 #ifndef MODEM_ABLATE_MIX
-            if (OUT_MODE != OUT_IQ_BASEBAND) {
-                float sn, cs;
-                sincos_phase(phase_from_f(p.w, idx_f32(nb + (double)(16 * r))), sn, cs);
-                z[r] = tx_cmix(z[r], (cf2){cs, sn});
-            }
-#endif
+        if (OUT_MODE != OUT_IQ_BASEBAND) {
+            // rows (0, 1) and (2, 3) as two packed phase pairs, side by side
+            const cf2 nf0 = (cf2){idx_f32(nb), idx_f32(nb + 16.0)};
+            const cf2 nf1 = (cf2){idx_f32(nb + 32.0), idx_f32(nb + 48.0)};
+            const cf2 ph0 = phase_from_f2(p.w, nf0), ph1 = phase_from_f2(p.w, nf1);
+            cf2 sn0, cs0, sn1, cs1;
+            sincos_phase2(ph0, sn0, cs0);
+            sincos_phase2(ph1, sn1, cs1);
+            z[0] = tx_cmix(z[0], (cf2){cs0.x, sn0.x});
+            z[1] = tx_cmix(z[1], (cf2){cs0.y, sn0.y});
+            z[2] = tx_cmix(z[2], (cf2){cs1.x, sn1.x});
+            z[3] = tx_cmix(z[3], (cf2){cs1.y, sn1.y});
         }
+#endif
 #ifdef MODEM_ABLATE_STORE
 #pragma unroll
         for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(z[r]));
