@@ -372,7 +372,7 @@ __device__ __forceinline__ cf2 cmix(cf2 x, cf2 cssn) {
     return z;
 #else
     const cf2 t = x * cssn.xx;
-    return __builtin_elementwise_fma((cf2){x.y, -x.x}, cssn.yy, t);
+    return __builtin_elementwise_fma(x.yx, (cf2){cssn.y, -cssn.y}, t);
 #endif
 }
 

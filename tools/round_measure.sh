@@ -17,7 +17,7 @@ cat "$out/bench.json"
 echo "[3/4] kernel trace"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
-    python3 "$root/bench.py" --steps 50 --warmup 10 --no-cpu-baseline > "$out/trace.log" 2>&1 || { tail -20 "$out/trace.log"; exit 3; }
+    python3 "$root/bench.py" --no-cpu-baseline > "$out/trace.log" 2>&1 || { tail -20 "$out/trace.log"; exit 3; }
 cd "$root"
 echo "[4/4] pmc"
 bash tools/pmc.sh "$out/pmc" c3 || exit 4
