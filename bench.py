@@ -62,11 +62,12 @@ def channel_seed(rank, nch, c):
 class GpuRunner:
     """The product path: rust_modem_amd handles on this rank's GPU, buffers resident in HBM."""
 
-    def __init__(self, wl, rank, device, streams=1):
+    def __init__(self, wl, rank, device, streams=1, batch=False):
         import torch
         import __graft_entry__ as g
         self.torch = torch
         m = g.package()
+        self._m = m
         name, bps, L, sps, nsamp, nch, dtype, _ = wl
         self.bps, self.L, self.sps, self.nsamp, self.nch, self.dtype = bps, L, sps, nsamp, nch, dtype
         torch.cuda.set_device(device)
@@ -75,6 +76,8 @@ class GpuRunner:
         # are queued on HIP stream c % streams, so the kernels of different channels overlap
         # (one channel's tail with the next one's head); stream 0 is the current stream
         self.streams = [self.stream] + [torch.cuda.Stream() for _ in range(max(1, streams) - 1)]
+        # or all channels through the batch entry points (one TX and one RX launch per step)
+        self.batch = batch
         taps = m.rrc_taps(L, sps, 0.35)
         w = m.Freq(1, 4).sample_freq()
         ph = {"qpsk": lambda: m.QPSK(0.0, 1.0), "qam16": lambda: m.QAM(4, 0.0, 1.0),
@@ -104,6 +107,13 @@ class GpuRunner:
         d["rx"].process(d["y"], out_iq=d["oiq"], out_sym=d["osym"], stream=stream)
 
     def step(self):
+        if self.batch:
+            m, ch = self._m, self.ch
+            m.DigitalModulator.process_batch([d["tx"] for d in ch], [d["bits"] for d in ch],
+                                             outs=[d["y"] for d in ch])
+            m.DemodulatorRx.process_batch([d["rx"] for d in ch], [d["y"] for d in ch],
+                                          out_iq=[d["oiq"] for d in ch], out_sym=[d["osym"] for d in ch])
+            return
         if len(self.streams) > 1:
             for st in self.streams[1:]:
                 st.wait_stream(self.stream)     # the step starts after what precedes it
@@ -257,6 +267,7 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
         "data": f"synthetic: splitmix64 bits (seed 0x5EED0000 + channel), one byte per bit, device-resident",
         "config": {"workload": desc, "samples_per_gpu_per_step": nsamp * nch, "channels_per_gpu": nch,
                    "streams_per_gpu": len(getattr(r, "streams", [None])),
+                   "channel_batch": bool(getattr(r, "batch", False)),
                    "ntaps": L, "sps": sps, "bits_per_symbol": bps, "rrc_beta": 0.35,
                    "carrier": "Freq::new(1, 4) (fs/4)", "parallelism": f"{world} independent channel set(s), "
                    "one per GPU, no collectives"},
@@ -305,6 +316,9 @@ def main(argv=None):
     # HIP streams the channels of a multi-channel config are spread over (0: one per channel,
     # at most 4 = the box's GPU_MAX_HW_QUEUES)
     ap.add_argument("--streams", type=int, default=0)
+    # multi-channel configs go through modem_*_process_batch (one launch for all channels of
+    # the step) unless --no-batch, which queues per-channel calls on --streams streams
+    ap.add_argument("--no-batch", action="store_true")
     args = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -316,8 +330,10 @@ def main(argv=None):
         torch.cuda.set_device(local)
         td.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         dist = _Dist(td, local)
-    nst = args.streams if args.streams > 0 else min(WORKLOADS[args.config][5], 4)
-    out = run(args, lambda wl, r: GpuRunner(wl, r, local, nst), dist, rank, world)
+    nch = WORKLOADS[args.config][5]
+    nst = args.streams if args.streams > 0 else min(nch, 4)
+    batch = nch > 1 and not args.no_batch
+    out = run(args, lambda wl, r: GpuRunner(wl, r, local, 1 if batch else nst, batch), dist, rank, world)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

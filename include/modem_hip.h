@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define MODEM_HIP_ABI_VERSION 2
+#define MODEM_HIP_ABI_VERSION 3
 
 typedef enum {
     MODEM_OK = 0,
@@ -192,6 +192,16 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
  * `cap` is in samples. */
 modem_status modem_tx_process(modem_tx* h, const uint8_t* bits, size_t nbits, void* out,
                               size_t cap, size_t* produced, void* stream);
+/* Several independent channels (distinct handles) in one call: the same results and handle
+ * states as modem_tx_process(hs[c], bits[c], nbits[c], outs[c], caps[c], &produced[c], stream)
+ * for c = 0 .. nch-1 in order. When every handle has the same matrix-core configuration
+ * (sps, taps, bits per symbol, mixed I/Q output of one dtype, device) and every buffer is
+ * device memory, up to 8 channels share one kernel launch; otherwise the calls run one by one.
+ * No reference counterpart (the reference drives one DigitalModulator per stream,
+ * modulator.rs:64-101): the multi-channel form of that loop, SURVEY.md §8e. */
+modem_status modem_tx_process_batch(modem_tx* const* hs, size_t nch, const uint8_t* const* bits,
+                                    const size_t* nbits, void* const* outs, const size_t* caps,
+                                    size_t* produced, void* stream);
 /* Append ceil((ntaps-1)/sps) all-zero symbols so the FIR tail drains. */
 modem_status modem_tx_flush(modem_tx* h, void* out, size_t cap, size_t* produced, void* stream);
 /* Samples that the next call will start at (Carrier.sample, carrier.rs:6). */
@@ -221,6 +231,14 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
  * this chunk. `cap` is in symbols. */
 modem_status modem_rx_process(modem_rx* h, const void* in, size_t n, void* out_iq,
                               uint8_t* out_sym, size_t cap, size_t* produced, void* stream);
+/* Several channels in one call, as modem_rx_process on each handle in order (out_iq[c] and
+ * out_sym[c] may be NULL). Fused into one launch per 8 channels when every handle has the
+ * same matrix-core configuration (decimation, taps, complex mix, one I/Q dtype in and out,
+ * device) and every buffer is device memory. The multi-channel form of Demodulator::next
+ * (demodulator.rs:44-56), SURVEY.md §8e. */
+modem_status modem_rx_process_batch(modem_rx* const* hs, size_t nch, const void* const* ins, const size_t* ns,
+                                    void* const* out_iq, uint8_t* const* out_sym, const size_t* caps,
+                                    size_t* produced, void* stream);
 /* Feed ntaps-1 zero samples (drains the matched filter). */
 modem_status modem_rx_flush(modem_rx* h, void* out_iq, uint8_t* out_sym, size_t cap,
                             size_t* produced, void* stream);

@@ -146,11 +146,15 @@ def load_library():
         "modem_tx_create": (st, [c.POINTER(_TxDesc), c.c_int, c.POINTER(vp)]),
         "modem_tx_process": (st, [vp, vp, sz, vp, sz, c.POINTER(sz), vp]),
         "modem_tx_flush": (st, [vp, vp, sz, c.POINTER(sz), vp]),
+        "modem_tx_process_batch": (st, [c.POINTER(vp), sz, c.POINTER(vp), c.POINTER(sz), c.POINTER(vp),
+                                        c.POINTER(sz), c.POINTER(sz), vp]),
         "modem_tx_sample": (u64, [vp]),
         "modem_tx_destroy": (st, [vp]),
         "modem_rx_create": (st, [c.POINTER(_RxDesc), c.c_int, c.POINTER(vp)]),
         "modem_rx_process": (st, [vp, vp, sz, vp, vp, sz, c.POINTER(sz), vp]),
         "modem_rx_flush": (st, [vp, vp, vp, sz, c.POINTER(sz), vp]),
+        "modem_rx_process_batch": (st, [c.POINTER(vp), sz, c.POINTER(vp), c.POINTER(sz), c.POINTER(vp),
+                                        c.POINTER(vp), c.POINTER(sz), c.POINTER(sz), vp]),
         "modem_rx_sample": (u64, [vp]),
         "modem_rx_destroy": (st, [vp]),
         "modem_fir_create": (st, [fp, u32, c.c_int, c.POINTER(vp)]),
@@ -581,6 +585,30 @@ class DigitalModulator:
         self.carrier.sample = int(load_library().modem_tx_sample(self._h))
         return out[: prod.value]
 
+    @staticmethod
+    def process_batch(mods, bits, outs=None, stream=None):
+        """`m.process(b)` for every (modulator, bits) pair in order, as one call
+        (modem_tx_process_batch): independent channels of one configuration with device
+        buffers share one kernel launch per 8 channels. Returns the outputs, as process does."""
+        mods, bits = list(mods), list(bits)
+        if len(mods) != len(bits) or len(set(map(id, mods))) != len(mods):
+            raise ValueError("one bits buffer per distinct modulator")
+        n = len(mods)
+        nb = [int(b.numel() if _is_torch(b) else b.size) for b in bits]
+        if outs is None:
+            outs = [m._alloc(b, m.nsamples(k)) for m, b, k in zip(mods, bits, nb)]
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        hs = (vp * n)(*[m._h.value for m in mods])
+        prod = (sz * n)()
+        _check(load_library().modem_tx_process_batch(
+            hs, n, (vp * n)(*[_ptr(b) for b in bits]), (sz * n)(*nb), (vp * n)(*[_ptr(o) for o in outs]),
+            (sz * n)(*[int(o.shape[0]) for o in outs]), prod, _stream_handle(stream)),
+            "DigitalModulator.process_batch")
+        for m, k in zip(mods, nb):
+            m._ncarry = (m._ncarry + k) % m.bps
+            m.carrier.sample = int(load_library().modem_tx_sample(m._h))
+        return [o[: prod[i]] for i, o in enumerate(outs)]
+
     def flush(self, like=None, stream=None):
         ntaps = 0 if self.taps is None else len(self.taps)
         tail = ntaps - 1 + self._q_offset if ntaps else 0     # the delayed Q rail drains later
@@ -656,6 +684,39 @@ class DemodulatorRx:
         self._consumed += n
         self.carrier.sample = int(load_library().modem_rx_sample(self._h))
         return (None if oiq is None else oiq[: prod.value]), (None if osym is None else osym[: prod.value])
+
+    @staticmethod
+    def process_batch(rxs, iqs, out_iq=None, out_sym=None, stream=None):
+        """`r.process(x)` for every (demodulator, input) pair in order, as one call
+        (modem_rx_process_batch): channels of one configuration with device buffers share one
+        kernel launch per 8 channels. Returns [(iq, sym), ...] as process does."""
+        rxs, iqs = list(rxs), list(iqs)
+        if len(rxs) != len(iqs) or len(set(map(id, rxs))) != len(rxs):
+            raise ValueError("one input buffer per distinct demodulator")
+        n = len(rxs)
+        ns = [int(x.shape[0]) for x in iqs]
+        nouts = [r.noutputs(k) for r, k in zip(rxs, ns)]
+        if out_iq is None:
+            out_iq = [_empty_like_input(x, (k, 2), np.float16 if r.out_dtype == DTYPE_F16 else np.float32)
+                      for r, x, k in zip(rxs, iqs, nouts)]
+        if out_sym is None:
+            out_sym = [_empty_like_input(x, (k,), np.uint8) if r._slicer is not None else None
+                       for r, x, k in zip(rxs, iqs, nouts)]
+        caps = [min(int(a.shape[0]) if a is not None else k, int(b.shape[0]) if b is not None else k)
+                for a, b, k in zip(out_iq, out_sym, nouts)]
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        prod = (sz * n)()
+        _check(load_library().modem_rx_process_batch(
+            (vp * n)(*[r._h.value for r in rxs]), n, (vp * n)(*[_ptr(x) for x in iqs]), (sz * n)(*ns),
+            (vp * n)(*[_ptr(a) or None for a in out_iq]), (vp * n)(*[_ptr(b) or None for b in out_sym]),
+            (sz * n)(*caps), prod, _stream_handle(stream)), "Demodulator.process_batch")
+        res = []
+        for i, (r, k) in enumerate(zip(rxs, ns)):
+            r._consumed += k
+            r.carrier.sample = int(load_library().modem_rx_sample(r._h))
+            a, b = out_iq[i], out_sym[i]
+            res.append((None if a is None else a[: prod[i]], None if b is None else b[: prod[i]]))
+        return res
 
     def flush(self, like=None, stream=None):
         n = len(self.taps) - 1

@@ -327,6 +327,7 @@ struct modem_tx {
     int hcur = 0, ccur = 0, ncarry = 0;
     int mfma_ksteps = 0;            // > 0: FIR on the matrix cores (tx_mfma)
     float* d_bfrag = nullptr;       // its split-f16 per-lane B fragments (modem_internal.h)
+    std::vector<_Float16> bfrag_host;   // the same, on the host (batch compatibility check)
     float* d_luth = nullptr;        // its split-f16 LUT (re_hi, re_lo, im_hi, im_lo per entry)
     int lut_scale_exp = 0, tap_scale_exp = 0;
     int levels = 0;                 // integer-level LUT (see TxParams)
@@ -519,6 +520,7 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
         const size_t nb = (bf.size() * sizeof(_Float16) + sizeof(float) - 1) / sizeof(float);
         const size_t nlh = (lh.size() * sizeof(_Float16) + sizeof(float) - 1) / sizeof(float);
         if ((st = dalloc(&h->d_bfrag, nb)) || (st = dalloc(&h->d_luth, nlh))) { delete h; return st; }
+        h->bfrag_host = bf;
         if (hipMemcpy(h->d_bfrag, bf.data(), bf.size() * sizeof(_Float16), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(h->d_luth, lh.data(), lh.size() * sizeof(_Float16), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipGetLastError();
@@ -530,33 +532,9 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     return MODEM_OK;
 }
 
-static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool flush, void* out,
-                           size_t cap, size_t* produced, hipStream_t s) {
-    if (!h || !produced || (nbits && !bits)) return MODEM_ERR_INVALID_ARG;
-    *produced = 0;
-    const uint64_t total = (uint64_t)h->ncarry + nbits;
-    const int64_t nsym = flush ? (int64_t)((h->ntaps ? h->ntaps - 1 + h->q_offset : 0) + h->sps - 1) / h->sps
-                               : (int64_t)(total / h->bps);
-    const int ncarry_new = flush ? h->ncarry : (int)(total - (uint64_t)nsym * h->bps);
-    const size_t nsamp = (size_t)nsym * h->sps;
-    if (nsamp > cap) return MODEM_ERR_CAPACITY;
-    if (nsamp && !out) return MODEM_ERR_INVALID_ARG;
-    DeviceGuard g(h->device);
-    if (!g.ok) return MODEM_ERR_NO_DEVICE;
-    modem_status st;
-    const uint8_t* dbits = bits;
-    if (nbits && !is_device_ptr(bits)) {
-        if ((st = h->bits_stage.ensure(nbits))) return st;
-        HIP_TRY(hipMemcpyAsync(h->bits_stage.p, bits, nbits, hipMemcpyHostToDevice, s));
-        dbits = static_cast<const uint8_t*>(h->bits_stage.p);
-    }
-    const bool host_out = nsamp && !is_device_ptr(out);
-    void* dout = out;
-    if (host_out) {
-        if ((st = h->out_stage.ensure(nsamp * tx_sample_bytes(h)))) return st;
-        dout = h->out_stage.p;
-    }
-    mk::TxParams p{};
+// Kernel parameters of one TX call on device buffers (dbits, dout); see tx_run.
+static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool flush, void* dout,
+                    int64_t nsym, int ncarry_new, size_t nsamp, mk::TxParams& p) {
     p.bits = dbits;
     p.carry = h->d_carry[h->ccur];
     p.carry_new = h->d_carry[h->ccur ^ 1];
@@ -596,6 +574,36 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     p.ph_shift = h->ph_shift;
     p.ph_map = h->ph_map;
     p.ph_max = h->ph_max;
+}
+
+static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool flush, void* out,
+                           size_t cap, size_t* produced, hipStream_t s) {
+    if (!h || !produced || (nbits && !bits)) return MODEM_ERR_INVALID_ARG;
+    *produced = 0;
+    const uint64_t total = (uint64_t)h->ncarry + nbits;
+    const int64_t nsym = flush ? (int64_t)((h->ntaps ? h->ntaps - 1 + h->q_offset : 0) + h->sps - 1) / h->sps
+                               : (int64_t)(total / h->bps);
+    const int ncarry_new = flush ? h->ncarry : (int)(total - (uint64_t)nsym * h->bps);
+    const size_t nsamp = (size_t)nsym * h->sps;
+    if (nsamp > cap) return MODEM_ERR_CAPACITY;
+    if (nsamp && !out) return MODEM_ERR_INVALID_ARG;
+    DeviceGuard g(h->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_status st;
+    const uint8_t* dbits = bits;
+    if (nbits && !is_device_ptr(bits)) {
+        if ((st = h->bits_stage.ensure(nbits))) return st;
+        HIP_TRY(hipMemcpyAsync(h->bits_stage.p, bits, nbits, hipMemcpyHostToDevice, s));
+        dbits = static_cast<const uint8_t*>(h->bits_stage.p);
+    }
+    const bool host_out = nsamp && !is_device_ptr(out);
+    void* dout = out;
+    if (host_out) {
+        if ((st = h->out_stage.ensure(nsamp * tx_sample_bytes(h)))) return st;
+        dout = h->out_stage.p;
+    }
+    mk::TxParams p{};
+    tx_fill(h, dbits, nbits, flush, dout, nsym, ncarry_new, nsamp, p);
     p.scan = nullptr;
     if (phasor_scanned(h->ph_kind)) {
         if ((st = h->scan_stage.ensure((size_t)std::max<int64_t>(nsym, 1) * sizeof(float2)))) return st;
@@ -628,6 +636,69 @@ modem_status modem_tx_process(modem_tx* h, const uint8_t* bits, size_t nbits, vo
 modem_status modem_tx_flush(modem_tx* h, void* out, size_t cap, size_t* produced, void* stream) {
     return tx_run(h, nullptr, 0, true, out, cap, produced, (hipStream_t)stream);
 }
+// One launch for several channels (independent channel streams). Equivalent to
+// modem_tx_process(hs[c], bits[c], nbits[c], outs[c], caps[c], &produced[c], stream) for
+// c = 0 .. nch-1 in order; fused into one launch per kBatchMax channels when every handle
+// shares the matrix-core configuration (sps, taps, bps, f32/f16 mixed I/Q output, device)
+// and all buffers are device memory, otherwise run one call at a time.
+modem_status modem_tx_process_batch(modem_tx* const* hs, size_t nch, const uint8_t* const* bits,
+                                    const size_t* nbits, void* const* outs, const size_t* caps,
+                                    size_t* produced, void* stream) {
+    if (nch == 0) return MODEM_OK;
+    if (!hs || !bits || !nbits || !outs || !caps || !produced) return MODEM_ERR_INVALID_ARG;
+    const hipStream_t s = (hipStream_t)stream;
+    bool fuse = nch >= 2 && hs[0] != nullptr;
+    for (size_t c = 0; fuse && c < nch; ++c) {
+        const modem_tx* h = hs[c];
+        const modem_tx* h0 = hs[0];
+        fuse = h && h->device == h0->device && h->ph_kind == 0 && h->mfma_ksteps > 0 &&
+               h->mfma_ksteps == h0->mfma_ksteps && h->out_mode == MODEM_OUT_IQ_MIXED && h->dtype == h0->dtype &&
+               h->sps == h0->sps && h->bps == h0->bps && h->ntaps == h0->ntaps && h->q_offset == 0 &&
+               h->bfrag_host == h0->bfrag_host && (nbits[c] == 0 || (bits[c] && is_device_ptr(bits[c]))) &&
+               outs[c] && is_device_ptr(outs[c]);
+        for (size_t e = 0; fuse && e < c; ++e) fuse = hs[e] != h;      // a handle at most once
+    }
+    if (!fuse) {
+        for (size_t c = 0; c < nch; ++c) {
+            const modem_status st = tx_run(hs[c], bits[c], nbits[c], false, outs[c], caps[c], &produced[c], s);
+            if (st != MODEM_OK) return st;
+        }
+        return MODEM_OK;
+    }
+    for (size_t c = 0; c < nch; ++c) produced[c] = 0;
+    // check every channel first: an error leaves all handles untouched
+    std::vector<int64_t> nsym(nch);
+    std::vector<int> ncarry_new(nch);
+    for (size_t c = 0; c < nch; ++c) {
+        const modem_tx* h = hs[c];
+        const uint64_t total = (uint64_t)h->ncarry + nbits[c];
+        nsym[c] = (int64_t)(total / h->bps);
+        ncarry_new[c] = (int)(total - (uint64_t)nsym[c] * h->bps);
+        if ((size_t)nsym[c] * h->sps > caps[c]) return MODEM_ERR_CAPACITY;
+    }
+    DeviceGuard g(hs[0]->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    for (size_t c0 = 0; c0 < nch; c0 += mk::kBatchMax) {
+        mk::TxBatch b{};
+        b.nch = (int32_t)std::min<size_t>(mk::kBatchMax, nch - c0);
+        for (int i = 0; i < b.nch; ++i) {
+            const size_t c = c0 + (size_t)i;
+            tx_fill(hs[c], bits[c], nbits[c], false, outs[c], nsym[c], ncarry_new[c], (size_t)nsym[c] * hs[c]->sps, b.p[i]);
+        }
+        HIP_TRY(mk::launch_tx_mfma_batch(b, (int)hs[0]->sps, hs[0]->mfma_ksteps, hs[0]->d_bfrag, hs[0]->dtype, s));
+        for (int i = 0; i < b.nch; ++i) {
+            const size_t c = c0 + (size_t)i;
+            modem_tx* h = hs[c];
+            h->hcur ^= 1;
+            h->ccur ^= 1;
+            h->ncarry = ncarry_new[c];
+            h->sample += (uint64_t)nsym[c] * h->sps;
+            h->symbols += (uint64_t)nsym[c];
+            produced[c] = (size_t)nsym[c] * h->sps;
+        }
+    }
+    return MODEM_OK;
+}
 uint64_t modem_tx_sample(const modem_tx* h) { return h ? h->sample : 0; }
 modem_status modem_tx_destroy(modem_tx* h) { delete h; return MODEM_OK; }
 
@@ -643,6 +714,7 @@ struct modem_rx {
     modem_slicer_desc slicer{};
     int mfma_ksteps = 0;            // > 0: matched filter on the matrix pipe (rx_mfma)
     float* d_bfrag = nullptr;       // its split-f16 tap tables (modem_internal.h)
+    std::vector<_Float16> bfrag_host;   // the same, on the host (batch compatibility check)
     int tap_scale_exp = 0;          // the tables hold h * 2^tap_scale_exp
     float* d_taps = nullptr;
     float2* d_slut = nullptr;
@@ -745,6 +817,7 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
             }
         const size_t nfl = (tab.size() * sizeof(_Float16) + sizeof(float) - 1) / sizeof(float);
         if ((st = dalloc(&h->d_bfrag, nfl))) { delete h; return st; }
+        h->bfrag_host = tab;
         if (hipMemcpy(h->d_bfrag, tab.data(), tab.size() * sizeof(_Float16), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
         }
@@ -761,6 +834,38 @@ static void rx_range(int64_t a, int64_t b, int64_t decim, int64_t D, int64_t* k0
     *k0 = first_at_or_after(a);
     const int64_t k1 = first_at_or_after(b);
     *cnt = k1 > *k0 ? k1 - *k0 : 0;
+}
+
+// Kernel parameters of one RX call on device buffers; see rx_run.
+static void rx_fill(const modem_rx* h, const void* din, size_t n, void* diq, uint8_t* dsym, int64_t k_first,
+                    int64_t nout, mk::RxParams& p) {
+    p.x = din;
+    p.hist = h->d_hist[h->hcur];
+    p.hist_new = h->d_hist[h->hcur ^ 1];
+    p.out_iq = nout ? diq : nullptr;
+    p.out_sym = nout ? dsym : nullptr;
+    p.taps = h->d_taps;
+    p.slut = h->d_slut;
+    p.N = (int64_t)n;
+    p.n_start = h->consumed;
+    p.c0 = h->c0;
+    p.k_first = k_first;
+    p.nout = nout;
+    p.K = (int)h->K;
+    p.L = (int)h->ntaps;
+    p.HL = (int)h->HL;
+    p.D = (int)h->D;
+    p.decim = (int)h->decim;
+    p.x_aligned16 = ((uintptr_t)din % 16) == 0 ? 1 : 0;
+    p.phase_offset = h->phase_offset;
+    p.exact_idx = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 53) ? 1 : 0;
+    p.slicer_kind = h->slicer.kind;
+    p.bps = (int)h->slicer.bits_per_symbol;
+    p.bits_per_carrier = (int)h->slicer.bits_per_carrier;
+    p.inv_scale = h->slicer.inv_scale;
+    p.max_symbol = h->slicer.max_symbol;
+    p.w = h->w;
+    p.tap_scale_exp = h->tap_scale_exp;
 }
 
 static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, void* out_iq,
@@ -792,33 +897,7 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
         dsym = static_cast<uint8_t*>(h->sym_stage.p);
     }
     mk::RxParams p{};
-    p.x = din;
-    p.hist = h->d_hist[h->hcur];
-    p.hist_new = h->d_hist[h->hcur ^ 1];
-    p.out_iq = nout ? diq : nullptr;
-    p.out_sym = nout ? dsym : nullptr;
-    p.taps = h->d_taps;
-    p.slut = h->d_slut;
-    p.N = (int64_t)n;
-    p.n_start = h->consumed;
-    p.c0 = h->c0;
-    p.k_first = k_first;
-    p.nout = nout;
-    p.K = (int)h->K;
-    p.L = (int)h->ntaps;
-    p.HL = (int)h->HL;
-    p.D = (int)h->D;
-    p.decim = (int)h->decim;
-    p.x_aligned16 = ((uintptr_t)din % 16) == 0 ? 1 : 0;
-    p.phase_offset = h->phase_offset;
-    p.exact_idx = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 53) ? 1 : 0;
-    p.slicer_kind = h->slicer.kind;
-    p.bps = (int)h->slicer.bits_per_symbol;
-    p.bits_per_carrier = (int)h->slicer.bits_per_carrier;
-    p.inv_scale = h->slicer.inv_scale;
-    p.max_symbol = h->slicer.max_symbol;
-    p.w = h->w;
-    p.tap_scale_exp = h->tap_scale_exp;
+    rx_fill(h, din, n, diq, dsym, k_first, nout, p);
     if (h->mfma_ksteps > 0)
         HIP_TRY(mk::launch_rx_mfma(p, (int)h->decim, h->mfma_ksteps, h->d_bfrag, h->in_dtype, h->out_dtype,
                                    h->mix, s));
@@ -841,6 +920,61 @@ modem_status modem_rx_flush(modem_rx* h, void* out_iq, uint8_t* out_sym, size_t 
                             void* stream) {
     if (!h) return MODEM_ERR_INVALID_ARG;
     return rx_run(h, nullptr, h->ntaps - 1, true, out_iq, out_sym, cap, produced, (hipStream_t)stream);
+}
+// One launch for several channels; equivalent to modem_rx_process on each in order. Fused
+// per kBatchMax channels when every handle shares the matrix-core configuration (decim,
+// taps, complex mix, one I/Q dtype in and out, device) and all buffers are device memory.
+modem_status modem_rx_process_batch(modem_rx* const* hs, size_t nch, const void* const* ins, const size_t* ns,
+                                    void* const* out_iq, uint8_t* const* out_sym, const size_t* caps,
+                                    size_t* produced, void* stream) {
+    if (nch == 0) return MODEM_OK;
+    if (!hs || !ins || !ns || !out_iq || !out_sym || !caps || !produced) return MODEM_ERR_INVALID_ARG;
+    const hipStream_t s = (hipStream_t)stream;
+    bool fuse = nch >= 2 && hs[0] != nullptr;
+    for (size_t c = 0; fuse && c < nch; ++c) {
+        const modem_rx* h = hs[c];
+        const modem_rx* h0 = hs[0];
+        fuse = h && h->device == h0->device && h->mfma_ksteps > 0 && h->mfma_ksteps == h0->mfma_ksteps &&
+               h->mix == MODEM_MIX_COMPLEX && h->in_dtype == h0->in_dtype && h->out_dtype == h->in_dtype &&
+               h->decim == h0->decim && h->ntaps == h0->ntaps && h->bfrag_host == h0->bfrag_host &&
+               (ns[c] == 0 || (ins[c] && is_device_ptr(ins[c]))) &&
+               (!out_iq[c] || is_device_ptr(out_iq[c])) && (!out_sym[c] || is_device_ptr(out_sym[c]));
+        for (size_t e = 0; fuse && e < c; ++e) fuse = hs[e] != h;
+    }
+    if (!fuse) {
+        for (size_t c = 0; c < nch; ++c) {
+            const modem_status st = rx_run(hs[c], ins[c], ns[c], false, out_iq[c], out_sym[c], caps[c],
+                                           &produced[c], s);
+            if (st != MODEM_OK) return st;
+        }
+        return MODEM_OK;
+    }
+    for (size_t c = 0; c < nch; ++c) produced[c] = 0;
+    std::vector<int64_t> k_first(nch), nout(nch);
+    for (size_t c = 0; c < nch; ++c) {
+        const modem_rx* h = hs[c];
+        rx_range(h->consumed, h->consumed + (int64_t)ns[c], h->decim, h->D, &k_first[c], &nout[c]);
+        if ((size_t)nout[c] > caps[c]) return MODEM_ERR_CAPACITY;
+    }
+    DeviceGuard g(hs[0]->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    for (size_t c0 = 0; c0 < nch; c0 += mk::kBatchMax) {
+        mk::RxBatch b{};
+        b.nch = (int32_t)std::min<size_t>(mk::kBatchMax, nch - c0);
+        for (int i = 0; i < b.nch; ++i) {
+            const size_t c = c0 + (size_t)i;
+            rx_fill(hs[c], ins[c], ns[c], out_iq[c], out_sym[c], k_first[c], nout[c], b.p[i]);
+        }
+        HIP_TRY(mk::launch_rx_mfma_batch(b, (int)hs[0]->decim, hs[0]->mfma_ksteps, hs[0]->d_bfrag,
+                                         hs[0]->in_dtype, s));
+        for (int i = 0; i < b.nch; ++i) {
+            const size_t c = c0 + (size_t)i;
+            hs[c]->hcur ^= 1;
+            hs[c]->consumed += (int64_t)ns[c];
+            produced[c] = (size_t)nout[c];
+        }
+    }
+    return MODEM_OK;
 }
 uint64_t modem_rx_sample(const modem_rx* h) { return h ? h->c0 + (uint64_t)h->consumed : 0; }
 modem_status modem_rx_destroy(modem_rx* h) { delete h; return MODEM_OK; }

@@ -112,6 +112,16 @@ hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStrea
 // TX FIR on the matrix cores (tx_mfma, split-f16 MFMA): 32-symbol k-steps for (sps, K), or 0
 // when no variant fits; bfrag = per-lane B fragments [ksteps][hi, lo][64 lanes][8 halves].
 int tx_mfma_ksteps(int sps, int K);
+// Channel batches (modem_tx_process_batch / modem_rx_process_batch): up to kBatchMax
+// independent handles of one configuration in one launch; the launcher sets g, the
+// workgroups per channel (workgroup b serves channel b / g).
+constexpr int kBatchMax = 8;
+struct TxBatch { TxParams p[kBatchMax]; int32_t nch; int32_t g; };
+struct RxBatch { RxParams p[kBatchMax]; int32_t nch; int32_t g; };
+// mixed-carrier I/Q output only (OUT_IQ_MIXED); dtype 0 f32, 1 f16
+hipError_t launch_tx_mfma_batch(const TxBatch& b, int sps, int nks, const void* bfrag, int dtype, hipStream_t s);
+// complex mix only (MIX_COMPLEX); in and out of one dtype
+hipError_t launch_rx_mfma_batch(const RxBatch& b, int decim, int nks, const void* tables, int dtype, hipStream_t s);
 hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const void* bfrag, int dtype,
                           int out_mode, hipStream_t s);
 // RX matched filter on the matrix cores (rx_mfma, split-f16 MFMA): 32-sample k-steps for

@@ -766,26 +766,27 @@ struct RxMfma {
 
 // (Capping this kernel at 4 waves/SIMD fits the steady loop in 128 registers but measured
 // slower on C3: 41.6 vs 35.7 us, with LDS still holding it at 3 workgroups per CU.)
+// One channel's share of a launch: workgroup `bid` of `nb` working on channel p.
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NT>::WPE)))
-void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
+__device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* __restrict__ tables,
+                                             int64_t bid, int64_t nb) {
     using K = RxMfma<DEC, NKS, InT, MIX, OutT, NT>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
     _Float16* pl = lds_h;                                   // 4 sample planes
     _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
     float* red = reinterpret_cast<float*>(tbl + K::NC * 2 * K::TB);
-    if (blockIdx.x == 0) rx_state_update<InT>(p);
+    if (bid == 0) rx_state_update<InT>(p);
     for (int j = threadIdx.x; j < K::NC * 2 * K::TB / 8; j += K::NT)
         reinterpret_cast<h8*>(tbl)[j] = reinterpret_cast<const h8*>(tables)[j];
     __syncthreads();
     const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;
-    const int64_t t0 = ntiles * blockIdx.x / gridDim.x, t1 = ntiles * (blockIdx.x + 1) / gridDim.x;
+    const int64_t t0 = ntiles * bid / nb, t1 = ntiles * (bid + 1) / nb;
     if (t0 >= t1) return;
 #ifdef MODEM_STAGGER
     // workgroups dealt to the same CU (b, b + CUs, ...) start a fraction of a tile apart so
     // their staging (VALU) and matrix phases interleave instead of running in lockstep
     {
-        const int k = (int)(blockIdx.x / (unsigned)MODEM_STAGGER) % 3;
+        const int k = (int)(bid / MODEM_STAGGER) % 3;
         for (int i = 0; i < k * 12; ++i) __builtin_amdgcn_s_sleep(127);   // ~8K cycles each step
     }
 #endif
@@ -798,6 +799,21 @@ void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
         if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, pl, tbl, red, t0, t1); return; }
     }
     K::template run<RXE_GEN>(p, pl, tbl, red, t0, t1);
+}
+
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NT>::WPE)))
+void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NT>(p, tables, blockIdx.x, gridDim.x);
+}
+
+// A batch of independent channels of one configuration (modem_rx_process_batch): workgroup
+// b serves channel b / g as its workgroup b % g of g.
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NT>::WPE)))
+void rx_mfma_batch(const RxBatch b, const _Float16* __restrict__ tables) {
+    const int ch = (int)(blockIdx.x / (unsigned)b.g);
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NT>(b.p[ch], tables, blockIdx.x - (unsigned)ch * b.g, b.g);
 }
 
 // Any decimation: thread per kept instant, mixed samples staged in natural order.
@@ -884,6 +900,25 @@ static hipError_t rxm_go(const RxParams& p, const void* tables, hipStream_t s) {
 #endif
 }
 
+template <int DEC, int NKS, typename InT, typename OutT>
+static hipError_t rxm_go_batch(RxBatch b, const void* tables, hipStream_t s) {
+    using K = RxMfma<DEC, NKS, InT, MIX_COMPLEX, OutT, 256>;
+    int64_t ntiles = 0;
+    for (int c = 0; c < b.nch; ++c) {
+        const int64_t t = (b.p[c].nout + (b.p[c].k_first & 15) + K::TS - 1) / K::TS;
+        ntiles = t > ntiles ? t : ntiles;
+    }
+    const size_t lds = K::LDS_BYTES;
+    const void* k = reinterpret_cast<const void*>(&rx_mfma_batch<DEC, NKS, InT, MIX_COMPLEX, OutT, 256>);
+    const int64_t cap = persistent_grid(k, K::NT, lds, INT64_MAX);
+    int64_t g = cap / b.nch;
+    g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
+    b.g = (int32_t)g;
+    hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX_COMPLEX, OutT, 256>), dim3((unsigned)(g * b.nch)),
+                       dim3(K::NT), lds, s, b, static_cast<const _Float16*>(tables));
+    return hipGetLastError();
+}
+
 // (decim, k-steps) variants: W = 32 * nks >= 15 * decim + ntaps.
 #ifdef MODEM_DEV_MIN      // experiment builds: the C3 variant only
 #define RXM_TABLE(X) X(4, 6)
@@ -897,6 +932,24 @@ static hipError_t rxm_sel(const RxParams& p, int decim, int nks, const void* tab
     RXM_TABLE(RXM)
 #undef RXM
     return hipErrorInvalidValue;
+}
+
+template <typename T>
+static hipError_t rxm_sel_batch(const RxBatch& b, int decim, int nks, const void* tables, hipStream_t s) {
+#define RXM(D, N) if (decim == D && nks == N) return rxm_go_batch<D, N, T, T>(b, tables, s);
+    RXM_TABLE(RXM)
+#undef RXM
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_rx_mfma_batch(const RxBatch& b, int decim, int nks, const void* tables, int dtype,
+                                hipStream_t s) {
+    if (b.nch < 1 || b.nch > kBatchMax) return hipErrorInvalidValue;
+#ifdef MODEM_DEV_MIN
+    if (dtype != 0) return hipErrorInvalidValue;
+    return rxm_sel_batch<float>(b, decim, nks, tables, s);
+#endif
+    return dtype == 1 ? rxm_sel_batch<__half>(b, decim, nks, tables, s) : rxm_sel_batch<float>(b, decim, nks, tables, s);
 }
 
 int rx_mfma_ksteps(int decim, int L) {

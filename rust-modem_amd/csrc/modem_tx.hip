@@ -548,14 +548,16 @@ struct TxMfma {
     }
 };
 
+// One channel's share of a launch: workgroup `bid` of `nb` working on channel p.
 template <int SPS, int NKS, int OUT_MODE, typename OutT>
-__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
+__device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __restrict__ bfrag,
+                                             int64_t bid, int64_t nb) {
     using K = TxMfma<SPS, NKS, OUT_MODE, OutT>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_t[];
     _Float16* pl = lds_t;
     th4* lut_s = reinterpret_cast<th4*>(lds_t + K::PLANES);
     const int tid = threadIdx.x, lane = tid & 63;
-    if (blockIdx.x == 0) tx_state_update(p);
+    if (bid == 0) tx_state_update(p);
     const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
     for (int i = tid; i < (1 << p.bps); i += K::NT) lut_s[i] = lut_h[i];
     th8 bh[NKS], bl[NKS];                        // this lane's B fragments (hi, lo) per k-step
@@ -566,9 +568,9 @@ __global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __re
     }
     __syncthreads();   // LUT visible
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
-    // tiles blockIdx.x, + gridDim.x, ...: concurrently running workgroups work on neighbouring
-    // tiles (measured 1 % faster on C3 than contiguous ranges per workgroup)
-    const int64_t t0 = blockIdx.x, t1 = ntiles, ts = gridDim.x;
+    // tiles bid, bid + nb, ...: concurrently running workgroups work on neighbouring tiles
+    // (measured 1 % faster on C3 than contiguous ranges per workgroup)
+    const int64_t t0 = bid, t1 = ntiles, ts = nb;
     if (t0 >= t1) return;
     if (p.fast_bits && p.exact_idx) {              // one uniform switch: the tile loop is specialised
         switch (p.bps) {
@@ -579,6 +581,19 @@ __global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __re
         }
     }
     K::template run<0>(p, pl, lut_s, bh, bl, t0, t1, ts);
+}
+
+template <int SPS, int NKS, int OUT_MODE, typename OutT>
+__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
+    tx_mfma_body<SPS, NKS, OUT_MODE, OutT>(p, bfrag, blockIdx.x, gridDim.x);
+}
+
+// A batch of independent channels of one configuration (modem_tx_process_batch): workgroup
+// b serves channel b / g as its workgroup b % g of g.
+template <int SPS, int NKS, int OUT_MODE, typename OutT>
+__global__ __launch_bounds__(256) void tx_mfma_batch(const TxBatch b, const th8* __restrict__ bfrag) {
+    const int ch = (int)(blockIdx.x / (unsigned)b.g);
+    tx_mfma_body<SPS, NKS, OUT_MODE, OutT>(b.p[ch], bfrag, blockIdx.x - (unsigned)ch * b.g, b.g);
 }
 
 // Any samples-per-symbol: thread per output sample, symbols staged in LDS.
@@ -800,6 +815,27 @@ static hipError_t txm_go(const TxParams& p, const void* bfrag, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Batch: g workgroups per channel, the persistent grid shared out over the channels (at least
+// one workgroup each, never more than the channel with the most tiles can use).
+template <int SPS, int NKS, int OM, typename OutT>
+static hipError_t txm_go_batch(TxBatch b, const void* bfrag, hipStream_t s) {
+    using K = TxMfma<SPS, NKS, OM, OutT>;
+    int64_t ntiles = 0;
+    for (int c = 0; c < b.nch; ++c) {
+        const int64_t t = (b.p[c].nsym + b.p[c].lead + K::TS - 1) / K::TS;
+        ntiles = t > ntiles ? t : ntiles;
+    }
+    const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << b.p[0].bps) * 8;
+    const void* k = reinterpret_cast<const void*>(&tx_mfma_batch<SPS, NKS, OM, OutT>);
+    const int64_t cap = persistent_grid(k, K::NT, lds, INT64_MAX);
+    int64_t g = cap / b.nch;
+    g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
+    b.g = (int32_t)g;
+    hipLaunchKernelGGL((tx_mfma_batch<SPS, NKS, OM, OutT>), dim3((unsigned)(g * b.nch)), dim3(K::NT), lds, s, b,
+                       static_cast<const th8*>(bfrag));
+    return hipGetLastError();
+}
+
 // (sps, k-steps) variants: W = 32 * nks >= 16/sps + K - 1 symbols (K = taps per phase).
 #ifdef MODEM_DEV_MIN      // experiment builds: the C3 variant only
 #define TXM_TABLE(X) X(4, 2)
@@ -814,6 +850,24 @@ static hipError_t txm_sel(const TxParams& p, int sps, int nks, const void* bfrag
     TXM_TABLE(TXM)
 #undef TXM
     return hipErrorInvalidValue;
+}
+
+template <typename OutT>
+static hipError_t txm_sel_batch(const TxBatch& b, int sps, int nks, const void* bfrag, hipStream_t s) {
+#define TXM(S, N) if (sps == S && nks == N) return txm_go_batch<S, N, OUT_IQ_MIXED, OutT>(b, bfrag, s);
+    TXM_TABLE(TXM)
+#undef TXM
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_tx_mfma_batch(const TxBatch& b, int sps, int nks, const void* bfrag, int dtype,
+                                hipStream_t s) {
+    if (b.nch < 1 || b.nch > kBatchMax) return hipErrorInvalidValue;
+#ifdef MODEM_DEV_MIN
+    if (dtype != 0) return hipErrorInvalidValue;
+    return txm_sel_batch<float>(b, sps, nks, bfrag, s);
+#endif
+    return dtype == 1 ? txm_sel_batch<__half>(b, sps, nks, bfrag, s) : txm_sel_batch<float>(b, sps, nks, bfrag, s);
 }
 
 int tx_mfma_ksteps(int sps, int K) {

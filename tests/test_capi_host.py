@@ -212,3 +212,15 @@ def test_modulate_cli_argument_panics():
     assert _cli(["-m", "qpsk", "-c", "900", "-p", "1"]) == 101   # sr % cf == 0 (modulate.rs:62)
     assert _cli(["-m", "msk"]) == 101                       # 45 samples/symbol: msk.rs:14
     assert _cli(["-h"]) == 0
+
+
+def test_batch_entry_argument_checks(m):
+    """modem_*_process_batch on the CPU: an empty batch is OK, missing arrays are INVALID_ARG
+    (no device is touched on either path)."""
+    L = m.load_library()
+    sz = ctypes.c_size_t
+    assert L.modem_tx_process_batch(None, 0, None, None, None, None, None, None) == 0
+    assert L.modem_rx_process_batch(None, 0, None, None, None, None, None, None, None) == 0
+    prod = (sz * 1)()
+    assert L.modem_tx_process_batch(None, 1, None, None, None, None, prod, None) == -1
+    assert L.modem_rx_process_batch(None, 1, None, None, None, None, None, prod, None) == -1

@@ -325,3 +325,56 @@ def test_errors_on_device(m, o, torch_cuda):
     out = torch_cuda.empty((3, 2), device="cuda")
     with pytest.raises(m.ModemError):     # 8 bits -> 4 symbols -> 16 samples > cap 3
         tx.process(torch_cuda.zeros(8, dtype=torch_cuda.uint8, device="cuda"), out=out)
+
+
+# ------------------------------------------------------------- channel batches ----
+@pytest.mark.parametrize("cfg,dtype", [("c2_qpsk", 0), ("c3_qam16", 0), ("c3_qam16", 1), ("c5_qam256", 0)])
+def test_batch_equals_single_calls(m, o, torch_cuda, cfg, dtype):
+    """process_batch (one launch per 8 channels) gives bit-identical samples, I/Q and
+    decisions to per-channel process() calls on separate handles, over two streaming calls;
+    10 channels with distinct carrier indices, ragged lengths and leftover bits exercise the
+    chunking (8 + 2), the per-channel state and the bit carry."""
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS[cfg]
+    taps = m.rrc_taps(L, sps, 0.35)
+    w = w_quarter(o)
+    nch = 10
+    s0s = [c * 1000003 + (c % 3) for c in range(nch)]
+
+    def mk(c):
+        tx = m.DigitalModulator(m.Carrier(w, s0s[c]), product_phasor(m, name), sps, taps, dtype=dtype)
+        rx = m.DemodulatorRx(m.Carrier(w, s0s[c]), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                             slicer=product_phasor(m, name).slicer(), in_dtype=dtype, out_dtype=dtype)
+        return tx, rx
+
+    single, batch = [mk(c) for c in range(nch)], [mk(c) for c in range(nch)]
+    for rnd in range(2):
+        bits = [torch.from_numpy(o.prng_bits(SEED + 200 + 10 * rnd + c, (1500 + 97 * c) * bps + c % bps)).cuda()
+                for c in range(nch)]
+        ys = [t.process(b) for (t, _), b in zip(single, bits)]
+        yb = m.DigitalModulator.process_batch([t for t, _ in batch], bits)
+        for c in range(nch):
+            assert yb[c].shape == ys[c].shape
+            assert torch.equal(yb[c], ys[c]), (rnd, c)
+            assert batch[c][0].carrier.sample == single[c][0].carrier.sample
+        rs = [r.process(y) for (_, r), y in zip(single, ys)]
+        rb = m.DemodulatorRx.process_batch([r for _, r in batch], yb)
+        for c in range(nch):
+            assert torch.equal(rb[c][0], rs[c][0]) and torch.equal(rb[c][1], rs[c][1]), (rnd, c)
+
+
+def test_batch_mixed_configs_fall_back(m, o, torch_cuda):
+    """Handles of different configurations in one batch run one call at a time, with the same
+    results as separate process() calls."""
+    torch = torch_cuda
+    w = w_quarter(o)
+    specs = [CONFIGS["c2_qpsk"], CONFIGS["c3_qam16"]]
+    mods, ref = [], []
+    for name, bps, L, sps in specs:
+        taps = m.rrc_taps(L, sps, 0.35)
+        mods.append(m.DigitalModulator(m.Carrier(w), product_phasor(m, name), sps, taps))
+        ref.append(m.DigitalModulator(m.Carrier(w), product_phasor(m, name), sps, taps))
+    bits = [torch.from_numpy(o.prng_bits(SEED + 300 + i, 2000 * bps)).cuda() for i, (_, bps, _, _) in enumerate(specs)]
+    yb = m.DigitalModulator.process_batch(mods, bits)
+    for i in range(2):
+        assert torch.equal(yb[i], ref[i].process(bits[i]))
