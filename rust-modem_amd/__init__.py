@@ -35,7 +35,7 @@ __all__ = [
     "BPSK", "QPSK", "QAM", "BASK", "MPSK", "APSK", "OQPSK",
     "rrc_taps", "DigitalModulator", "DemodulatorRx", "FIRFilter", "prng_bits",
     "MIX_COMPLEX", "MIX_REFERENCE_REAL", "OUT_IQ_MIXED", "OUT_IQ_BASEBAND", "OUT_REAL",
-    "SLICER_NONE", "SLICER_NEAREST", "SLICER_QAM_AXIS", "DTYPE_F32", "DTYPE_F16",
+    "TxBatchPlan", "RxBatchPlan", "SLICER_NONE", "SLICER_NEAREST", "SLICER_QAM_AXIS", "DTYPE_F32", "DTYPE_F16",
 ]
 
 PI32 = float(np.float32(math.pi))      # std::f32::consts::PI
@@ -627,6 +627,38 @@ class DigitalModulator:
             self._h = None
 
 
+class TxBatchPlan:
+    """A prepared `DigitalModulator.process_batch` over fixed buffers: bits[c] -> outs[c] for
+    every channel, the ctypes argument arrays built once, so that each `run()` is one C call
+    (modem_tx_process_batch) plus the per-channel bookkeeping. For a channel bank that streams
+    through the same device buffers every period."""
+
+    def __init__(self, mods, bits, outs):
+        self.mods, self.bits, self.outs = list(mods), list(bits), list(outs)
+        n = self.n = len(self.mods)
+        if len(self.bits) != n or len(self.outs) != n or len(set(map(id, self.mods))) != n:
+            raise ValueError("one bits and one output buffer per distinct modulator")
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        self._nb = [int(b.numel() if _is_torch(b) else b.size) for b in self.bits]
+        self._hs = (vp * n)(*[m._h.value for m in self.mods])
+        self._bits = (vp * n)(*[_ptr(b) for b in self.bits])
+        self._nbits = (sz * n)(*self._nb)
+        self._outs = (vp * n)(*[_ptr(o) for o in self.outs])
+        self._caps = (sz * n)(*[int(o.shape[0]) for o in self.outs])
+        self._prod = (sz * n)()
+        self._fn = load_library().modem_tx_process_batch
+
+    def run(self, stream=None):
+        """Returns the samples produced per channel (written to outs[c][:produced[c]])."""
+        _check(self._fn(self._hs, self.n, self._bits, self._nbits, self._outs, self._caps, self._prod,
+                        _stream_handle(stream)), "TxBatchPlan.run")
+        L = load_library()
+        for m, k in zip(self.mods, self._nb):
+            m._ncarry = (m._ncarry + k) % m.bps
+            m.carrier.sample = int(L.modem_tx_sample(m._h))
+        return list(self._prod)
+
+
 # ------------------------------------------------------------------- RX (B6+B5) ----
 class DemodulatorRx:
     """Demodulator (demodulator.rs:7-56) + matched filter + decimation + slicer.
@@ -804,6 +836,40 @@ class FIRFilter:
         if getattr(self, "_h", None) and _lib is not None:
             _lib.modem_fir_destroy(self._h)
             self._h = None
+
+
+class RxBatchPlan:
+    """A prepared `DemodulatorRx.process_batch` over fixed buffers (iqs[c] -> out_iq[c],
+    out_sym[c]; either output may be None): each `run()` is one modem_rx_process_batch call."""
+
+    def __init__(self, rxs, iqs, out_iq, out_sym):
+        self.rxs, self.iqs = list(rxs), list(iqs)
+        n = self.n = len(self.rxs)
+        out_iq, out_sym = list(out_iq), list(out_sym)
+        if len(self.iqs) != n or len(out_iq) != n or len(out_sym) != n or len(set(map(id, self.rxs))) != n:
+            raise ValueError("one input and one output set per distinct demodulator")
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        self._ns = [int(x.shape[0]) for x in self.iqs]
+        caps = [min(int(a.shape[0]) if a is not None else 1 << 62, int(b.shape[0]) if b is not None else 1 << 62)
+                for a, b in zip(out_iq, out_sym)]
+        self._hs = (vp * n)(*[r._h.value for r in self.rxs])
+        self._ins = (vp * n)(*[_ptr(x) for x in self.iqs])
+        self._nsa = (sz * n)(*self._ns)
+        self._oiq = (vp * n)(*[_ptr(a) or None for a in out_iq])
+        self._osym = (vp * n)(*[_ptr(b) or None for b in out_sym])
+        self._caps = (sz * n)(*caps)
+        self._prod = (sz * n)()
+        self._fn = load_library().modem_rx_process_batch
+
+    def run(self, stream=None):
+        """Returns the kept instants produced per channel."""
+        _check(self._fn(self._hs, self.n, self._ins, self._nsa, self._oiq, self._osym, self._caps, self._prod,
+                        _stream_handle(stream)), "RxBatchPlan.run")
+        L = load_library()
+        for r, k in zip(self.rxs, self._ns):
+            r._consumed += k
+            r.carrier.sample = int(L.modem_rx_sample(r._h))
+        return list(self._prod)
 
 
 def prng_bits(seed: int, nbits: int, device: int = 0, stream=None):

@@ -95,16 +95,9 @@ __device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t nb, int off,
     return make_float2(__builtin_fmaf(x.y, s, x.x * c), __builtin_fmaf(-x.x, s, x.y * c));
 }
 
-__device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float im) {
+// Nearest LUT entry, lowest index on ties (squared distance, no contraction).
+__device__ __forceinline__ uint8_t rx_slice_nearest(const RxParams& p, float re, float im) {
 #pragma clang fp contract(off)
-    if (p.slicer_kind == SLICER_QAM_AXIS) {
-        const int ms = (int)p.max_symbol;
-        const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
-        const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
-        const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), (float)ms);
-        const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), (float)ms);
-        return (uint8_t)((si << p.bits_per_carrier) | sq);
-    }
     cfloat* lut = (cfloat*)p.slut;
     const int n = 1 << p.bps;
     uint32_t best = 0;
@@ -115,6 +108,19 @@ __device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float i
         if (d < bd) { bd = d; best = (uint32_t)k; }
     }
     return (uint8_t)best;
+}
+
+__device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    if (p.slicer_kind == SLICER_QAM_AXIS) {
+        const int ms = (int)p.max_symbol;
+        const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
+        const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
+        const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), (float)ms);
+        const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), (float)ms);
+        return (uint8_t)((si << p.bits_per_carrier) | sq);
+    }
+    return rx_slice_nearest(p, re, im);
 }
 
 template <typename OutT>
@@ -333,7 +339,7 @@ __host__ __device__ constexpr int rxh_pos(int e, int RW) { return e + 16 * (e / 
 
 // What the steady-state epilogue writes: baseband IQ, QAM-axis decisions, or both
 // (RXE_GEN: any other combination, guarded per store).
-enum { RXE_GEN = 0, RXE_IQ = 1, RXE_SYM = 2, RXE_IQSYM = 3 };
+enum { RXE_GEN = 0, RXE_IQ = 1, RXE_SYM = 2, RXE_IQSYM = 3, RXE_NEAREST = 4 };   // | NEAREST: LUT slicer
 
 __device__ __forceinline__ uint8_t rx_slice_qam(const RxParams& p, float re, float im) {
 #pragma clang fp contract(off)
@@ -670,7 +676,7 @@ struct RxMfma {
                 continue;
             }
             if (EM & RXE_IQ) OutIO<OutT>::store_one(qb, off, re, im);
-            if (EM & RXE_SYM) sb[off] = rx_slice_qam(p, re, im);
+            if (EM & RXE_SYM) sb[off] = (EM & RXE_NEAREST) ? rx_slice_nearest(p, re, im) : rx_slice_qam(p, re, im);
         }
     }
 
@@ -795,8 +801,18 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     if (std::is_same<InT, float>::value && MIX == MIX_COMPLEX) {
         const bool qam = p.slicer_kind == SLICER_QAM_AXIS && p.out_sym;
         if (p.out_iq && qam) { K::template run<RXE_IQSYM>(p, pl, tbl, red, t0, t1); return; }
+        if (p.out_iq && p.out_sym && p.slicer_kind == SLICER_NEAREST) {
+            K::template run<RXE_IQSYM | RXE_NEAREST>(p, pl, tbl, red, t0, t1);
+            return;
+        }
         if (p.out_iq && !p.out_sym) { K::template run<RXE_IQ>(p, pl, tbl, red, t0, t1); return; }
         if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, pl, tbl, red, t0, t1); return; }
+    }
+    // f16 storage of the loopback chain (C5 f16): I/Q and QAM decisions, unconditional stores
+    if (std::is_same<InT, __half>::value && MIX == MIX_COMPLEX && p.out_iq && p.out_sym &&
+        p.slicer_kind == SLICER_QAM_AXIS) {
+        K::template run<RXE_IQSYM>(p, pl, tbl, red, t0, t1);
+        return;
     }
     K::template run<RXE_GEN>(p, pl, tbl, red, t0, t1);
 }
@@ -812,8 +828,15 @@ void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NT>::WPE)))
 void rx_mfma_batch(const RxBatch b, const _Float16* __restrict__ tables) {
+#ifdef MODEM_BATCH_INTERLEAVE
+    const int ch = (int)(blockIdx.x % (unsigned)b.nch);
+    const unsigned bid = blockIdx.x / (unsigned)b.nch;
+#else
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NT>(b.p[ch], tables, blockIdx.x - (unsigned)ch * b.g, b.g);
+    const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
+#endif
+    const RxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NT>(p, tables, bid, b.g);
 }
 
 // Any decimation: thread per kept instant, mixed samples staged in natural order.

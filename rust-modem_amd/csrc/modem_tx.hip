@@ -592,8 +592,15 @@ __global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __re
 // b serves channel b / g as its workgroup b % g of g.
 template <int SPS, int NKS, int OUT_MODE, typename OutT>
 __global__ __launch_bounds__(256) void tx_mfma_batch(const TxBatch b, const th8* __restrict__ bfrag) {
+#ifdef MODEM_BATCH_INTERLEAVE
+    const int ch = (int)(blockIdx.x % (unsigned)b.nch);
+    const unsigned bid = blockIdx.x / (unsigned)b.nch;
+#else
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
-    tx_mfma_body<SPS, NKS, OUT_MODE, OutT>(b.p[ch], bfrag, blockIdx.x - (unsigned)ch * b.g, b.g);
+    const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
+#endif
+    const TxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
+    tx_mfma_body<SPS, NKS, OUT_MODE, OutT>(p, bfrag, bid, b.g);
 }
 
 // Any samples-per-symbol: thread per output sample, symbols staged in LDS.

@@ -333,7 +333,8 @@ def test_batch_equals_single_calls(m, o, torch_cuda, cfg, dtype):
     """process_batch (one launch per 8 channels) gives bit-identical samples, I/Q and
     decisions to per-channel process() calls on separate handles, over two streaming calls;
     10 channels with distinct carrier indices, ragged lengths and leftover bits exercise the
-    chunking (8 + 2), the per-channel state and the bit carry."""
+    chunking (8 + 2), the per-channel state and the bit carry (one channel's first call is
+    shorter than a symbol: it produces nothing and only carries its bits)."""
     torch = torch_cuda
     name, bps, L, sps = CONFIGS[cfg]
     taps = m.rrc_taps(L, sps, 0.35)
@@ -349,8 +350,9 @@ def test_batch_equals_single_calls(m, o, torch_cuda, cfg, dtype):
 
     single, batch = [mk(c) for c in range(nch)], [mk(c) for c in range(nch)]
     for rnd in range(2):
-        bits = [torch.from_numpy(o.prng_bits(SEED + 200 + 10 * rnd + c, (1500 + 97 * c) * bps + c % bps)).cuda()
-                for c in range(nch)]
+        # channel 0 gets fewer bits than one symbol in the first call (no samples, only carry)
+        nb = [(bps - 1 if (rnd == 0 and c == 0) else (1500 + 97 * c) * bps + c % bps) for c in range(nch)]
+        bits = [torch.from_numpy(o.prng_bits(SEED + 200 + 10 * rnd + c, nb[c])).cuda() for c in range(nch)]
         ys = [t.process(b) for (t, _), b in zip(single, bits)]
         yb = m.DigitalModulator.process_batch([t for t, _ in batch], bits)
         for c in range(nch):
@@ -378,3 +380,37 @@ def test_batch_mixed_configs_fall_back(m, o, torch_cuda):
     yb = m.DigitalModulator.process_batch(mods, bits)
     for i in range(2):
         assert torch.equal(yb[i], ref[i].process(bits[i]))
+
+
+def test_batch_plans_equal_single_calls(m, o, torch_cuda):
+    """TxBatchPlan / RxBatchPlan (prepared batch calls over fixed buffers, run every period)
+    give the same samples, I/Q and decisions as per-channel process() calls, period after
+    period."""
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS["c3_qam16"]
+    taps = m.rrc_taps(L, sps, 0.35)
+    w = w_quarter(o)
+    nch, nsym = 3, 2048
+
+    def mk(c):
+        tx = m.DigitalModulator(m.Carrier(w, 777 * c), product_phasor(m, name), sps, taps)
+        rx = m.DemodulatorRx(m.Carrier(w, 777 * c), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                             slicer=product_phasor(m, name).slicer())
+        return tx, rx
+
+    single, batch = [mk(c) for c in range(nch)], [mk(c) for c in range(nch)]
+    bits = [torch.from_numpy(o.prng_bits(SEED + 400 + c, nsym * bps)).cuda() for c in range(nch)]
+    ys = [torch.empty((nsym * sps, 2), device="cuda") for _ in range(nch)]
+    iqs = [torch.empty((nsym, 2), device="cuda") for _ in range(nch)]
+    syms = [torch.empty(nsym, dtype=torch.uint8, device="cuda") for _ in range(nch)]
+    txp = m.TxBatchPlan([t for t, _ in batch], bits, ys)
+    rxp = m.RxBatchPlan([r for _, r in batch], ys, iqs, syms)
+    for period in range(3):
+        assert txp.run() == [nsym * sps] * nch
+        got = rxp.run()
+        for c in range(nch):
+            y = single[c][0].process(bits[c])
+            assert torch.equal(ys[c], y), (period, c)
+            giq, gsym = single[c][1].process(y)
+            assert got[c] == giq.shape[0]
+            assert torch.equal(iqs[c][: got[c]], giq) and torch.equal(syms[c][: got[c]], gsym), (period, c)
