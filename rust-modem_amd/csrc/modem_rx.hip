@@ -110,6 +110,22 @@ __device__ __forceinline__ uint8_t rx_slice_nearest(const RxParams& p, float re,
     return (uint8_t)best;
 }
 
+// The same for a 4-entry LUT (QPSK), unrolled: the table stays in scalar registers across
+// the tile loop instead of being re-read per decision.
+__device__ __forceinline__ uint8_t rx_slice_nearest4(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    cfloat* lut = (cfloat*)p.slut;
+    uint32_t best = 0;
+    float bd = __builtin_inff();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float dr = re - lut[2 * k], di = im - lut[2 * k + 1];
+        const float d = dr * dr + di * di;
+        if (d < bd) { bd = d; best = (uint32_t)k; }
+    }
+    return (uint8_t)best;
+}
+
 __device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float im) {
 #pragma clang fp contract(off)
     if (p.slicer_kind == SLICER_QAM_AXIS) {
@@ -676,7 +692,9 @@ struct RxMfma {
                 continue;
             }
             if (EM & RXE_IQ) OutIO<OutT>::store_one(qb, off, re, im);
-            if (EM & RXE_SYM) sb[off] = (EM & RXE_NEAREST) ? rx_slice_nearest(p, re, im) : rx_slice_qam(p, re, im);
+            if (EM & RXE_SYM)
+                sb[off] = !(EM & RXE_NEAREST) ? rx_slice_qam(p, re, im)
+                        : p.bps == 2 ? rx_slice_nearest4(p, re, im) : rx_slice_nearest(p, re, im);
         }
     }
 
