@@ -404,7 +404,13 @@ template <> struct Quad<float> {
     struct T { float4 a, b; };
     __device__ static T load(const void* x, int64_t q) {      // q: sample index (8-B aligned)
         const float4* v = reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(x) + q);
+#ifdef MODEM_RX_NT_LOAD
+        const f32x4* w = reinterpret_cast<const f32x4*>(v);
+        const f32x4 a = __builtin_nontemporal_load(w), b = __builtin_nontemporal_load(w + 1);
+        return T{make_float4(a[0], a[1], a[2], a[3]), make_float4(b[0], b[1], b[2], b[3])};
+#else
         return T{v[0], v[1]};
+#endif
     }
     __device__ static void split(const T& t, float2 (&x)[4]) {
         x[0] = make_float2(t.a.x, t.a.y); x[1] = make_float2(t.a.z, t.a.w);

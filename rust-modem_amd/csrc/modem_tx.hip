@@ -455,6 +455,12 @@ struct TxMfma {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             char* q = ob + (uint32_t)((loff + 16 * r) * SBYTES);
+#ifdef MODEM_TX_NT_STORE
+            if (OUT_MODE != OUT_REAL && std::is_same<OutT, float>::value) {
+                __builtin_nontemporal_store(z[r], reinterpret_cast<cf2*>(q));
+                continue;
+            }
+#endif
             if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(q, 0, z[r].x);
             else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
         }
