@@ -193,25 +193,54 @@ class GpuRunner:
         return bool(torch.equal(got, sent[idx]))
 
 
-def cpu_baseline(wl, nsamp_cpu):
-    """The CPU oracle (reference loop structure, C, 1 thread) on a bounded sample of the batch."""
+def _cpu_threads():
+    """Host threads for the multi-core leg: the CPUs this process may run on, at most 16 (the
+    GPU box's CPU share per GPU; nproc there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(wl, nsamp_cpu, threads=None):
+    """The CPU oracle (the reference loop structure restated in C) on a bounded sample of the
+    workload: one thread on `nsamp_cpu` samples, then `threads` threads on independent channels
+    (seed + c, as the GPU channels) of nsamp_cpu / 2 samples each, as SURVEY.md §8d asks (the
+    ctypes calls release the GIL, so the threads run the C loop in parallel). The reported
+    value is the multi-core rate; the single-thread rate is kept beside it."""
     import __graft_entry__ as g
+    from concurrent.futures import ThreadPoolExecutor
     o = g.oracle()
     name, bps, L, sps = wl[0], wl[1], wl[2], wl[3]
-    p = {"qpsk": lambda: o.new_phasor(o.QPSK, 0.0, 1.0), "qam16": lambda: o.new_phasor(o.QAM, 4, 0.0, 1.0),
-         "qam256": lambda: o.new_phasor(o.QAM, 8, 0.0, 1.0)}[name]()
     taps = o.rrc_taps(L, sps, 0.35)
     w = o.sample_freq(1, 4)
-    bits = o.prng_bits(SEED, nsamp_cpu // sps * bps)
-    sl = o.qam_axis_slicer(bps, 1.0) if name.startswith("qam") else \
-        o.make_slicer(o.SLICER_NEAREST, bps, o.phasor_lut(p))
+
+    def chain(seed, nsamp):
+        p = {"qpsk": lambda: o.new_phasor(o.QPSK, 0.0, 1.0), "qam16": lambda: o.new_phasor(o.QAM, 4, 0.0, 1.0),
+             "qam256": lambda: o.new_phasor(o.QAM, 8, 0.0, 1.0)}[name]()
+        sl = o.qam_axis_slicer(bps, 1.0) if name.startswith("qam") else \
+            o.make_slicer(o.SLICER_NEAREST, bps, o.phasor_lut(p))
+        bits = o.prng_bits(seed, nsamp // sps * bps)
+        y = o.tx_chain(p, bits, sps, taps, w, 0)
+        o.rx_chain(y, w, 0, o.MIX_COMPLEX, taps, sps, L - 1, sl)
+        return len(y)
+
     t0 = time.perf_counter()
-    y = o.tx_chain(p, bits, sps, taps, w, 0)
-    _, sym = o.rx_chain(y, w, 0, o.MIX_COMPLEX, taps, sps, L - 1, sl)
-    dt = time.perf_counter() - t0
-    return {"value": round(len(y) / dt / 1e6, 4), "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": f"{len(y)} samples ({len(y) // sps} symbols) of the same workload, TX+RX oracle "
-                      f"loop (per-sample FIRFilter at full rate, glibc sin/cos), 1 thread, {dt:.1f} s",
+    n1 = chain(SEED, nsamp_cpu)
+    dt1 = time.perf_counter() - t0
+    T = threads or _cpu_threads()
+    per = max(sps, nsamp_cpu // 2 // sps * sps)
+    with ThreadPoolExecutor(T) as ex:
+        t0 = time.perf_counter()
+        nt = sum(ex.map(lambda c: chain(SEED + c, per), range(T)))
+        dtT = time.perf_counter() - t0
+    return {"value": round(nt / dtT / 1e6, 4), "unit": "Msamples/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x {per} samples ({per // sps} symbols) of the same workload on independent "
+                      f"channels, TX+RX oracle loop (per-sample FIRFilter at full rate, glibc sin/cos), "
+                      f"{dtT:.1f} s",
+            "single_thread": {"value": round(n1 / dt1 / 1e6, 4), "cores": 1,
+                              "sample": f"{n1} samples ({n1 // sps} symbols), {dt1:.1f} s"},
             "cpu": _cpu_model()}
 
 
