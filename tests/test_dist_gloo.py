@@ -96,3 +96,15 @@ def test_two_ranks_gloo(tmp_path):
     assert abs(outs[0]["value"] - total / (outs[0]["ms_per_step"] * 3 / 1e3) / 1e6) <= 0.02 * outs[0]["value"]
     # ranks own disjoint channels
     assert not set(outs[0]["_seeds"]) & set(outs[1]["_seeds"])
+
+
+def test_cpu_baseline_multicore_leg():
+    """bench.cpu_baseline: the single-thread leg plus the threaded leg over independent
+    channels (seed + c), bounded sample, with the thread count it used in `cores`."""
+    import bench
+    out = bench.cpu_baseline(bench.WORKLOADS["c3"], 1 << 14, threads=2)
+    assert out["kind"] == "port" and out["unit"] == "Msamples/s"
+    assert out["cores"] == 2 and out["value"] > 0
+    assert out["single_thread"]["cores"] == 1 and out["single_thread"]["value"] > 0
+    assert "2 threads x 8192 samples" in out["sample"]
+    assert 1 <= bench._cpu_threads() <= 16
