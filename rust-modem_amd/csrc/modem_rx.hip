@@ -453,6 +453,9 @@ __device__ __forceinline__ int tile_scale_exp(float lane_max, float* red) {
     return 141 - ex;                                        // max * 2^k in [2^14, 2^15)
 }
 
+// The tiles one workgroup runs, in order: first, first + step, ... (count of them).
+struct TileSeq { int64_t first, step, count; };
+
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NTT>
 struct RxMfma {
     using C = RxMfmaCfg<DEC, NTT>;
@@ -714,8 +717,8 @@ struct RxMfma {
         }
     }
 
-    // Tiles of [t0, t1) (a contiguous range per workgroup: measured 9 % faster on C3 than
-    // handing neighbouring tiles to concurrently running workgroups, and dynamic tile handout
+    // The tiles of `sq` (the XCD-matched top-down rounds of rx_mfma_body; a contiguous range
+    // per workgroup measured 9 % faster on C3 than bottom-up rounds, and dynamic tile handout
     // through per-XCD atomic counters did not beat it either). When the input is 8-B aligned
     // and the carrier indices stay below 2^53, the run of "full" tiles (all staged samples
     // inside the chunk, all 1024 instants kept) goes through the prefetched loop, whose
@@ -723,7 +726,7 @@ struct RxMfma {
     // general path.
     template <int EM>
     __device__ static void run(const RxParams& p, _Float16* pl, const _Float16* tbl, float* red,
-                               int64_t t0, int64_t t1) {
+                               const TileSeq sq) {
         const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar
         // quad loads need dword alignment only (16-B loads at 8-B aligned sample offsets)
         const bool fast = p.exact_idx && ((uintptr_t)p.x & 3) == 0;
@@ -738,8 +741,8 @@ struct RxMfma {
         // next tile is restaged). The epilogue's stores stay unconditional, so the next trip's
         // vmcnt waits remain counted.
         auto clamped_base = [&](int64_t t) {
-            const int64_t base = q_lo_of(p, t);
-            return base > p.N - 4 * NQ ? p.N - 4 * NQ : base;
+            const int64_t base = q_lo_of(p, t);   // (the first tile of a call may start before 0)
+            return base > p.N - 4 * NQ ? p.N - 4 * NQ : base < 0 ? 0 : base;
         };
         auto prefetch = [&](int64_t t) {
             const int64_t base = clamped_base(t);
@@ -749,13 +752,13 @@ struct RxMfma {
             for (int u = 0; u < U; ++u)                     // the partial last slot: its waves only
                 if ((u + 1) * NT <= NQ || 64 * wave + NT * u < NQ) pre[u] = load_slot(p, base, l0, u);
         };
-        int64_t t = t0;
+        int64_t i = 0, t = sq.first;
         bool restage = false;
         STAMP_DECL;
-        while (t < t1) {
+        while (i < sq.count) {
             if (full(t) && !restage) {
                 prefetch(t);
-                for (; t < t1 && full(t); ++t) {
+                for (; i < sq.count && full(t); ++i, t += sq.step) {
                     const int64_t n_lo = q_lo_of(p, t) + p.n_start;
 #ifdef MODEM_STAMPS
                     STAMP(0);                              // loop overhead
@@ -766,7 +769,7 @@ struct RxMfma {
                     STAMP(2);                              // staging + tile-max barrier
                     if (ka != 0) { restage = true; break; }       // uniform; leaves the loop
                     // (the tile-max reduction in stage_fast ended with a barrier: planes visible)
-                    if (t + 1 < t1) prefetch(t + 1);       // next samples fly during the MFMAs
+                    if (i + 1 < sq.count) prefetch(t + sq.step);   // next samples fly during the MFMAs
                     STAMP(3);                              // prefetch issue
                     f32x4 dre, dim;
                     fir(pl, tbl, dre, dim);
@@ -785,7 +788,8 @@ struct RxMfma {
                 fir(pl, tbl, dre, dim);
                 emit_edge(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
                 __syncthreads();
-                ++t;
+                ++i;
+                t += sq.step;
                 STAMP(7);                                  // general-path tiles
             }
         }
@@ -810,8 +814,23 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
         reinterpret_cast<h8*>(tbl)[j] = reinterpret_cast<const h8*>(tables)[j];
     __syncthreads();
     const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;
+#ifndef MODEM_RX_CONTIG
+    // Rounds of nb tiles from the top down, tile R - (r + 1) nb + bid in round r. The TX hands
+    // its tiles out grid-strided (tile i to workgroup i mod grid, both grids multiples of 8, so
+    // tile i is written on XCD slot i mod 8); the RX's first round then reads the ~32 MiB the
+    // TX wrote last, each tile on the XCD slot that wrote it (blocks b and b + 8 share an XCD).
+    // C3: 35.0 -> 33.8 us, A/B twice on one box against contiguous ranges per workgroup
+    // (MODEM_RX_CONTIG; that variant now spills 28 B/lane, 37-38 us). PMC FETCH_SIZE per launch
+    // is unchanged (139 vs 137 MB), so the gain is not fewer L2 misses but where the misses are
+    // served from (the most recently written lines, still in the memory-side cache).
+    const int64_t R = (ntiles + nb - 1) / nb * nb;
+    TileSeq sq{R - nb + bid, -nb, R / nb};
+    if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }
+#else
     const int64_t t0 = ntiles * bid / nb, t1 = ntiles * (bid + 1) / nb;
-    if (t0 >= t1) return;
+    const TileSeq sq{t0, 1, t1 - t0};
+#endif
+    if (sq.count <= 0) return;
 #ifdef MODEM_STAGGER
     // workgroups dealt to the same CU (b, b + CUs, ...) start a fraction of a tile apart so
     // their staging (VALU) and matrix phases interleave instead of running in lockstep
@@ -824,21 +843,21 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     // it stores, so the tile loop's store count is static. Other variants share the guarded one.
     if (std::is_same<InT, float>::value && MIX == MIX_COMPLEX) {
         const bool qam = p.slicer_kind == SLICER_QAM_AXIS && p.out_sym;
-        if (p.out_iq && qam) { K::template run<RXE_IQSYM>(p, pl, tbl, red, t0, t1); return; }
+        if (p.out_iq && qam) { K::template run<RXE_IQSYM>(p, pl, tbl, red, sq); return; }
         if (p.out_iq && p.out_sym && p.slicer_kind == SLICER_NEAREST) {
-            K::template run<RXE_IQSYM | RXE_NEAREST>(p, pl, tbl, red, t0, t1);
+            K::template run<RXE_IQSYM | RXE_NEAREST>(p, pl, tbl, red, sq);
             return;
         }
-        if (p.out_iq && !p.out_sym) { K::template run<RXE_IQ>(p, pl, tbl, red, t0, t1); return; }
-        if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, pl, tbl, red, t0, t1); return; }
+        if (p.out_iq && !p.out_sym) { K::template run<RXE_IQ>(p, pl, tbl, red, sq); return; }
+        if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, pl, tbl, red, sq); return; }
     }
     // f16 storage of the loopback chain (C5 f16): I/Q and QAM decisions, unconditional stores
     if (std::is_same<InT, __half>::value && MIX == MIX_COMPLEX && p.out_iq && p.out_sym &&
         p.slicer_kind == SLICER_QAM_AXIS) {
-        K::template run<RXE_IQSYM>(p, pl, tbl, red, t0, t1);
+        K::template run<RXE_IQSYM>(p, pl, tbl, red, sq);
         return;
     }
-    K::template run<RXE_GEN>(p, pl, tbl, red, t0, t1);
+    K::template run<RXE_GEN>(p, pl, tbl, red, sq);
 }
 
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
