@@ -820,11 +820,15 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     // tile i is written on XCD slot i mod 8); the RX's first round then reads the ~32 MiB the
     // TX wrote last, each tile on the XCD slot that wrote it (blocks b and b + 8 share an XCD).
     // C3: 35.0 -> 33.8 us, A/B twice on one box against contiguous ranges per workgroup
-    // (MODEM_RX_CONTIG; that variant now spills 28 B/lane, 37-38 us). PMC FETCH_SIZE per launch
-    // is unchanged (139 vs 137 MB), so the gain is not fewer L2 misses but where the misses are
-    // served from (the most recently written lines, still in the memory-side cache).
+    // (MODEM_RX_CONTIG; that variant now spills 28 B/lane, 37-38 us). The XCD match is what
+    // pays: the same rounds with the slots shifted by 1 or 4 (MODEM_RX_XCD_SHIFT) measured
+    // 38.1-39.1 us. PMC FETCH_SIZE per launch is unchanged (139 vs 137 MB).
     const int64_t R = (ntiles + nb - 1) / nb * nb;
+#ifdef MODEM_RX_XCD_SHIFT     // experiment: the same rounds with the XCD slots mismatched
+    TileSeq sq{R - nb + (bid + MODEM_RX_XCD_SHIFT) % nb, -nb, R / nb};
+#else
     TileSeq sq{R - nb + bid, -nb, R / nb};
+#endif
     if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }
 #else
     const int64_t t0 = ntiles * bid / nb, t1 = ntiles * (bid + 1) / nb;
