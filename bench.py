@@ -62,7 +62,7 @@ def channel_seed(rank, nch, c):
 class GpuRunner:
     """The product path: rust_modem_amd handles on this rank's GPU, buffers resident in HBM."""
 
-    def __init__(self, wl, rank, device, streams=1, batch=False):
+    def __init__(self, wl, rank, device, streams=1, batch=False, amplitude=1.0):
         import torch
         import __graft_entry__ as g
         self.torch = torch
@@ -80,8 +80,10 @@ class GpuRunner:
         self.batch = batch
         taps = m.rrc_taps(L, sps, 0.35)
         w = m.Freq(1, 4).sample_freq()
-        ph = {"qpsk": lambda: m.QPSK(0.0, 1.0), "qam16": lambda: m.QAM(4, 0.0, 1.0),
-              "qam256": lambda: m.QAM(8, 0.0, 1.0)}[name]
+        # amplitude != 1 scales the constellation (and with it the RX input and the slicer)
+        A = float(amplitude)
+        ph = {"qpsk": lambda: m.QPSK(0.0, A), "qam16": lambda: m.QAM(4, 0.0, A),
+              "qam256": lambda: m.QAM(8, 0.0, A)}[name]
         self.ch = []
         nbits = nsamp // sps * bps
         for c in range(nch):
@@ -142,37 +144,37 @@ class GpuRunner:
             self.tx(0)
             self.rx(0)
 
-    def kernel_times_ms(self, reps, rounds=5):
-        """Mean device time of one TX and one RX launch, from HIP events on the launch stream
-        (channel 0's launches, or the batch launches that cover every channel).
+    def _rx_all(self):
+        if self.batch:
+            self._rxp.run()
+        else:
+            self.rx(0)
 
-        Events between every pair of kernels add their own gaps, so the chain is timed as
-        `reps` back-to-back TX+RX steps between two events, TX alone as `reps` back-to-back TX
-        launches, and RX as the difference. Untimed steps are queued first so that the device
-        has a backlog (events recorded while it waits for the host would time the host). The
-        pair is measured `rounds` times, interleaved, and the medians are reported (a single
-        round swings by a few us with the clocks)."""
+    def kernel_times_ms(self, reps, rounds=5):
+        """Mean device time of one TX launch, one RX launch and one TX+RX step, from HIP events
+        on the launch stream (channel 0's launches, or the batch launches that cover every
+        channel). Each is timed directly as `reps` back-to-back launches between two events:
+        TX alone, RX alone (re-reading the sample buffer the last TX wrote, resident in HBM),
+        and the chain. Untimed launches are queued first so that the device has a backlog
+        (events recorded while it waits for the host would time the host). The three are
+        measured `rounds` times, interleaved, and the medians are reported (a single round
+        swings by a few us with the clocks)."""
         torch = self.torch
-        chain, tx = [], []
+        res = {"tx": [], "rx": [], "chain": []}
+        legs = (("chain", self._step_timed), ("tx", self._tx_all), ("rx", self._rx_all))
         for _ in range(rounds):
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-            for _ in range(16):
-                self._step_timed()
-            ev[0].record(self.stream)
-            for _ in range(reps):
-                self._step_timed()
-            ev[1].record(self.stream)
-            for _ in range(8):
-                self._tx_all()
-            ev[2].record(self.stream)
-            for _ in range(reps):
-                self._tx_all()
-            ev[3].record(self.stream)
-            torch.cuda.synchronize()
-            chain.append(ev[0].elapsed_time(ev[1]) / reps)
-            tx.append(ev[2].elapsed_time(ev[3]) / reps)
-        t_chain, t_tx = sorted(chain)[rounds // 2], sorted(tx)[rounds // 2]
-        return t_tx, t_chain - t_tx
+            for name, fn in legs:
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                for _ in range(8):
+                    fn()
+                ev[0].record(self.stream)
+                for _ in range(reps):
+                    fn()
+                ev[1].record(self.stream)
+                torch.cuda.synchronize()
+                res[name].append(ev[0].elapsed_time(ev[1]) / reps)
+        med = {k: sorted(v)[rounds // 2] for k, v in res.items()}
+        return med["tx"], med["rx"], med["chain"]
 
     def check(self):
         """Decisions of channel 0 equal the symbols sent (size-independent parity property)."""
@@ -288,7 +290,7 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
     total = nsamp * nch * args.steps * world
     value = total / dt / 1e6
     ok = r.check()
-    t_tx, t_rx = r.kernel_times_ms(max(10, min(args.steps, 50)))
+    t_tx, t_rx, t_chain = r.kernel_times_ms(max(20, min(args.steps, 100)))
     b_tx, b_rx, nout = algorithmic_bytes(bps, L, sps, nsamp, dtype)
     per_launch = nch if getattr(r, "batch", False) else 1      # channels one timed launch covers
     b_tx, b_rx, nsamp_launch = b_tx * per_launch, b_rx * per_launch, nsamp * per_launch
@@ -296,7 +298,7 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
     achieved = dom[2] / (dom[1] * 1e-3) / 1e9
     traffic = pmc_traffic(args.config)
     dom_traffic = traffic.get(dom[0]) if isinstance(traffic, dict) else None
-    chain_gbs = (b_tx + b_rx) / ((t_tx + t_rx) * 1e-3) / 1e9
+    chain_gbs = (b_tx + b_rx) / (t_chain * 1e-3) / 1e9
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -319,15 +321,42 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
         "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": dom_traffic,
                      "algorithmic_bytes_per_launch": dom[2], "mean_launch_ms": round(dom[1], 5)},
-        "chain_roofline": {"tx_ms": round(t_tx, 5), "rx_ms": round(t_rx, 5), "tx_bytes": b_tx, "rx_bytes": b_rx,
-                           "bytes_per_sample": round((b_tx + b_rx) / nsamp, 4),
+        "chain_roofline": {"tx_ms": round(t_tx, 5), "rx_ms": round(t_rx, 5), "chain_ms": round(t_chain, 5),
+                           "tx_bytes": b_tx, "rx_bytes": b_rx,
+                           "bytes_per_sample": round((b_tx + b_rx) / nsamp_launch, 4),
                            "achieved": round(chain_gbs, 1), "frac": round(chain_gbs / HBM_PEAK_GBS, 4),
-                           "device_msamples_per_s": round(nsamp_launch / ((t_tx + t_rx) * 1e-3) / 1e6, 1)},
+                           "device_msamples_per_s": round(nsamp_launch / (t_chain * 1e-3) / 1e6, 1)},
         "decisions_match_sent": ok,
     }
+    if args.amplitude != 1.0:
+        out["config"]["amplitude"] = args.amplitude
+    if rank == 0 and world == 1 and args.config == "c3" and not args.no_out_of_cache:
+        del r
+        out["roofline_out_of_cache"] = out_of_cache_roofline(runner_factory)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, args.cpu_samples)
     return out
+
+
+def out_of_cache_roofline(runner_factory, config="c5"):
+    """The C3 chain's 2^24-sample working set (~180 MB) fits the 256 MiB Infinity Cache, whose
+    hits FETCH_SIZE and the roofline count like HBM reads; C5 f32 (512 MiB of samples) does
+    not. Its RX launch and chain, timed the same way, give the out-of-cache figure."""
+    wl = WORKLOADS[config]
+    name, bps, L, sps, nsamp, nch, dtype, desc = wl
+    r = runner_factory(wl, 0)
+    for _ in range(3):
+        r.step()
+    r.sync()
+    t_tx, t_rx, t_chain = r.kernel_times_ms(10, rounds=3)
+    b_tx, b_rx, _ = algorithmic_bytes(bps, L, sps, nsamp, dtype)
+    rx_gbs = b_rx / (t_rx * 1e-3) / 1e9
+    chain_gbs = (b_tx + b_rx) / (t_chain * 1e-3) / 1e9
+    return {"workload": desc, "kernel": "rx", "achieved": round(rx_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(rx_gbs / HBM_PEAK_GBS, 4), "mean_launch_ms": round(t_rx, 5),
+            "algorithmic_bytes_per_launch": b_rx, "tx_ms": round(t_tx, 5), "chain_ms": round(t_chain, 5),
+            "chain_frac": round(chain_gbs / HBM_PEAK_GBS, 4),
+            "chain_msamples_per_s": round(nsamp / (t_chain * 1e-3) / 1e6, 1)}
 
 
 class _Dist:
@@ -364,6 +393,10 @@ def main(argv=None):
     # multi-channel configs go through modem_*_process_batch (one launch for all channels of
     # the step) unless --no-batch, which queues per-channel calls on --streams streams
     ap.add_argument("--no-batch", action="store_true")
+    # constellation amplitude (1.0 = BASELINE); e.g. 1/16 puts the RX input below 2^-3
+    ap.add_argument("--amplitude", type=float, default=1.0)
+    # skip the C5 f32 out-of-Infinity-Cache roofline measured after the C3 line
+    ap.add_argument("--no-out-of-cache", action="store_true")
     args = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -378,7 +411,8 @@ def main(argv=None):
     nch = WORKLOADS[args.config][5]
     nst = args.streams if args.streams > 0 else min(nch, 4)
     batch = nch > 1 and not args.no_batch
-    out = run(args, lambda wl, r: GpuRunner(wl, r, local, 1 if batch else nst, batch), dist, rank, world)
+    out = run(args, lambda wl, r: GpuRunner(wl, r, local, 1 if batch else nst, batch, args.amplitude),
+              dist, rank, world)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

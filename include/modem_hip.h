@@ -36,7 +36,8 @@
  *     carrier sample counter, the FIR history, leftover bits and the decimation phase);
  *     `*_flush` drains the filter with zeros.
  *   - One handle = one device; a handle is not thread-safe (it mirrors `&mut self`);
- *     distinct handles may be driven from different host threads.
+ *     distinct handles may be driven from different host threads. Device buffers passed to
+ *     a handle must live on that handle's device (another GPU's memory: INVALID_ARG).
  */
 #ifndef MODEM_HIP_H
 #define MODEM_HIP_H
@@ -48,7 +49,9 @@
 extern "C" {
 #endif
 
-#define MODEM_HIP_ABI_VERSION 3
+/* 2: modem_tx_desc.q_offset; 3: the channel-batch entry points; 4: modem_rx_desc.phase_offset
+ * (the descriptor grew 8 bytes: 80 -> 88) and modem_pll_lock. Layouts: INTEGRATION.md. */
+#define MODEM_HIP_ABI_VERSION 4
 
 typedef enum {
     MODEM_OK = 0,

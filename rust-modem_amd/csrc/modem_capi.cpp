@@ -41,6 +41,16 @@ bool is_device_ptr(const void* p) {
     return a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
 }
 
+// Device memory of a GPU other than `dev` (managed memory is reachable from every device).
+// A handle's kernels run on its own device: such a buffer would be read over the fabric or
+// fault, so the entry points refuse it (the reference has one address space, no counterpart).
+bool foreign_ptr(const void* p, int dev) {
+    if (!p) return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return a.type == hipMemoryTypeDevice && a.device != dev;
+}
+
 #define HIP_TRY(expr)                                                              \
     do {                                                                           \
         if ((expr) != hipSuccess) { (void)hipGetLastError(); return MODEM_ERR_HIP; } \
@@ -233,7 +243,7 @@ modem_status modem_rates_sps(uint64_t br, uint64_t sr, uint64_t* sps) {   // rat
 float modem_carrier_phase(float w, uint64_t n) { return mod_trig(w * (float)n); }   // carrier.rs:17-19
 
 modem_status modem_carrier_phases(float w, uint64_t s0, size_t n, float* out, int device, void* stream) {
-    if (n && (!out || !is_device_ptr(out))) return MODEM_ERR_INVALID_ARG;
+    if (n && (!out || !is_device_ptr(out) || foreign_ptr(out, device))) return MODEM_ERR_INVALID_ARG;
     if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
     DeviceGuard g(device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
@@ -587,6 +597,8 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     const size_t nsamp = (size_t)nsym * h->sps;
     if (nsamp > cap) return MODEM_ERR_CAPACITY;
     if (nsamp && !out) return MODEM_ERR_INVALID_ARG;
+    if ((nbits && foreign_ptr(bits, h->device)) || (nsamp && foreign_ptr(out, h->device)))
+        return MODEM_ERR_INVALID_ARG;
     DeviceGuard g(h->device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     modem_status st;
@@ -647,6 +659,9 @@ modem_status modem_tx_process_batch(modem_tx* const* hs, size_t nch, const uint8
     if (nch == 0) return MODEM_OK;
     if (!hs || !bits || !nbits || !outs || !caps || !produced) return MODEM_ERR_INVALID_ARG;
     const hipStream_t s = (hipStream_t)stream;
+    for (size_t c = 0; c < nch; ++c)    // an error leaves every handle untouched
+        if (hs[c] && ((nbits[c] && foreign_ptr(bits[c], hs[c]->device)) || foreign_ptr(outs[c], hs[c]->device)))
+            return MODEM_ERR_INVALID_ARG;
     bool fuse = nch >= 2 && hs[0] != nullptr;
     for (size_t c = 0; fuse && c < nch; ++c) {
         const modem_tx* h = hs[c];
@@ -719,12 +734,13 @@ struct modem_rx {
     float* d_taps = nullptr;
     float2* d_slut = nullptr;
     void* d_hist[2] = {nullptr, nullptr};
+    int* d_ka = nullptr;            // rx_mfma staging-exponent prediction, double-buffered like d_hist
     void* d_zeros = nullptr;
     int hcur = 0;
     Stage in_stage, iq_stage, sym_stage;
     ~modem_rx() {
         DeviceGuard g(device);
-        for (void* p : {(void*)d_taps, (void*)d_slut, d_hist[0], d_hist[1], d_zeros, (void*)d_bfrag})
+        for (void* p : {(void*)d_taps, (void*)d_slut, d_hist[0], d_hist[1], d_zeros, (void*)d_bfrag, (void*)d_ka})
             if (p) (void)hipFree(p);
     }
 };
@@ -779,7 +795,10 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
         return st;
     }
     h->d_hist[0] = h0; h->d_hist[1] = h1; h->d_zeros = z;
-    if (hipMemcpy(h->d_taps, pp.data(), pp.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+    const int ka_none[2] = {INT32_MIN, INT32_MIN};
+    if ((st = dalloc(&h->d_ka, 2))) { delete h; return st; }
+    if (hipMemcpy(h->d_taps, pp.data(), pp.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->d_ka, ka_none, sizeof ka_none, hipMemcpyHostToDevice) != hipSuccess) {
         (void)hipGetLastError(); delete h; return MODEM_ERR_HIP;
     }
     if (sl.kind == MODEM_SLICER_NEAREST &&
@@ -859,6 +878,9 @@ static void rx_fill(const modem_rx* h, const void* din, size_t n, void* diq, uin
     p.x_aligned16 = ((uintptr_t)din % 16) == 0 ? 1 : 0;
     p.phase_offset = h->phase_offset;
     p.exact_idx = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 53) ? 1 : 0;
+    p.idx46 = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL + 65536) < (1ull << 46) ? 1 : 0;
+    p.ka_in = h->d_ka + h->hcur;
+    p.ka_out = h->d_ka + (h->hcur ^ 1);
     p.slicer_kind = h->slicer.kind;
     p.bps = (int)h->slicer.bits_per_symbol;
     p.bits_per_carrier = (int)h->slicer.bits_per_carrier;
@@ -875,6 +897,9 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
     int64_t k_first, nout;
     rx_range(h->consumed, h->consumed + (int64_t)n, h->decim, h->D, &k_first, &nout);
     if ((size_t)nout > cap) return MODEM_ERR_CAPACITY;
+    if ((n && !zeros && foreign_ptr(in, h->device)) || (nout && foreign_ptr(out_iq, h->device)) ||
+        (nout && foreign_ptr(out_sym, h->device)))
+        return MODEM_ERR_INVALID_ARG;
     DeviceGuard g(h->device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     modem_status st;
@@ -930,6 +955,10 @@ modem_status modem_rx_process_batch(modem_rx* const* hs, size_t nch, const void*
     if (nch == 0) return MODEM_OK;
     if (!hs || !ins || !ns || !out_iq || !out_sym || !caps || !produced) return MODEM_ERR_INVALID_ARG;
     const hipStream_t s = (hipStream_t)stream;
+    for (size_t c = 0; c < nch; ++c)
+        if (hs[c] && ((ns[c] && foreign_ptr(ins[c], hs[c]->device)) || foreign_ptr(out_iq[c], hs[c]->device) ||
+                      foreign_ptr(out_sym[c], hs[c]->device)))
+            return MODEM_ERR_INVALID_ARG;
     bool fuse = nch >= 2 && hs[0] != nullptr;
     for (size_t c = 0; fuse && c < nch; ++c) {
         const modem_rx* h = hs[c];
@@ -1016,6 +1045,7 @@ modem_status modem_fir_create(const float* taps, uint32_t ntaps, int device, mod
 
 modem_status modem_fir_process(modem_fir* h, const float* in, float* out, size_t n, void* stream) {
     if (!h || (n && (!in || !out))) return MODEM_ERR_INVALID_ARG;
+    if (n && (foreign_ptr(in, h->device) || foreign_ptr(out, h->device))) return MODEM_ERR_INVALID_ARG;
     DeviceGuard g(h->device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     hipStream_t s = (hipStream_t)stream;
@@ -1051,7 +1081,7 @@ modem_status modem_fir_destroy(modem_fir* h) { delete h; return MODEM_OK; }
 
 modem_status modem_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, int device, void* stream) {
     if (nbits && !out) return MODEM_ERR_INVALID_ARG;
-    if (nbits && !is_device_ptr(out)) return MODEM_ERR_INVALID_ARG;
+    if (nbits && (!is_device_ptr(out) || foreign_ptr(out, device))) return MODEM_ERR_INVALID_ARG;
     if (!device_ok(device)) return MODEM_ERR_NO_DEVICE;
     DeviceGuard g(device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;

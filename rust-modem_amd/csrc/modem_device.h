@@ -278,34 +278,4 @@ __device__ __forceinline__ void mfma_chain_lb(const float2* arow, OffF off, cons
     }
 }
 
-
-// ------------------------------------------------------------- diagnostic stamps ----
-// MODEM_STAMPS builds only (tools/stamps.py): per-wave cycle sums of a tile loop's segments,
-// accumulated in scalar registers and stored once by lane 0 into g_stamps (a buffer no other
-// code reads). Never compiled into the product library.
-#ifdef MODEM_STAMPS
-constexpr int kStampSegs = 12;   // 8 segment sums, then realtime at entry / exit, spare
-static __device__ unsigned long long g_stamps[4096 * 4 * kStampSegs];
-__device__ __forceinline__ unsigned long long stamp_now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-__device__ __forceinline__ unsigned long long stamp_real() {
-    unsigned long long t;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-    return t;
-}
-#define STAMP_DECL unsigned long long st_sum[kStampSegs] = {0}, st_last = stamp_now(); st_sum[8] = stamp_real()
-#define STAMP(k) do { const unsigned long long t_ = stamp_now(); st_sum[k] += t_ - st_last; st_last = t_; } while (0)
-#define STAMP_FLUSH(slot) do { st_sum[9] = stamp_real(); if ((threadIdx.x & 63) == 0) \
-    for (int k_ = 0; k_ < kStampSegs; ++k_) g_stamps[(size_t)(slot) * kStampSegs + k_] = st_sum[k_]; } while (0)
-#else
-#define STAMP_DECL do {} while (0)
-#define STAMP(k) do {} while (0)
-#define STAMP_FLUSH(slot) do {} while (0)
-#endif
-
 }  // namespace mk

@@ -91,6 +91,9 @@ struct RxParams {
     float w;
     int32_t tap_scale_exp;   // rx_mfma: tables hold h * 2^tap_scale_exp
     float phase_offset;      // PLL offset added to the carrier phase (demodulator.rs:50)
+    int32_t idx46;           // every carrier index of this call is < 2^46 (rx_mfma's f32 index split)
+    const int* ka_in;        // rx_mfma: staging exponent the previous call ended with (INT_MIN: none)
+    int* ka_out;             // rx_mfma: the one this call ends with (workgroup 0's last tile)
 };
 
 struct FirParams {

@@ -84,13 +84,23 @@ __device__ __forceinline__ float rx_phase(const RxParams& p, float carrier) {
     return carrier + p.phase_offset;
 }
 
+// sin / cos of carrier.next() + pll.phase_offset (demodulator.rs:50) on the hardware
+// v_sin/v_cos (argument in turns): turns = fma(carrier, 1/2pi, offset/2pi), the same
+// expression in every RX path (fast, general, VALU), so that results never depend on which
+// path a sample took. For offset 0 it is fl(carrier / 2pi) exactly as __sinf/__cosf take it.
+__device__ __forceinline__ void rx_sincos(const RxParams& p, float carrier, float& s, float& c) {
+    const float rev = __builtin_fmaf(carrier, kRcp2Pi, p.phase_offset * kRcp2Pi);
+    s = __builtin_amdgcn_sinf(rev);
+    c = __builtin_amdgcn_cosf(rev);
+}
+
 // x * e^{-j phase} (or the reference's x.re * (cos, -sin), demodulator.rs:46,53-54) for
 // stream index n = nb + off (nb wave-uniform).
 template <int MIX>
 __device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t nb, int off, float2 x) {
     if (nb + off < 0) return make_float2(0.f, 0.f);   // before the stream: zero history
     float s, c;
-    sincos_phase(rx_phase(p, carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.exact_idx)), s, c);
+    rx_sincos(p, carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.exact_idx), s, c);
     if (MIX == MIX_REFERENCE_REAL) return make_float2(x.x * c, x.x * -s);
     return make_float2(__builtin_fmaf(x.y, s, x.x * c), __builtin_fmaf(-x.x, s, x.y * c));
 }
@@ -132,8 +142,9 @@ __device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float i
         const int ms = (int)p.max_symbol;
         const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
         const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
-        const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), (float)ms);
-        const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), (float)ms);
+        const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), p.max_symbol);
+        const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), p.max_symbol);
+        (void)ms;
         return (uint8_t)((si << p.bits_per_carrier) | sq);
     }
     return rx_slice_nearest(p, re, im);
@@ -141,10 +152,6 @@ __device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float i
 
 template <typename OutT>
 __device__ __forceinline__ void rx_emit(const RxParams& p, int64_t o, float re, float im) {
-#ifdef MODEM_ABLATE_STORE
-    asm volatile("" :: "v"(re), "v"(im));
-    return;
-#endif
     if (p.out_iq) OutIO<OutT>::store_one(p.out_iq, o, re, im);
     if (p.out_sym && p.slicer_kind != SLICER_NONE) p.out_sym[o] = rx_slice(p, re, im);
 }
@@ -216,11 +223,7 @@ __device__ __forceinline__ void rx_stage_fast(const RxParams& p, float2* lds, in
             const int e = el + 2 * NT * u;
             if (e >= 0 && e < NS) {
                 float s, c;
-#ifdef MODEM_ABLATE_MIX
-                s = 0.f; c = idx_f32(lb + (double)(j + 2 * NT * u));
-#else
-                sincos_phase(rx_phase(p, phase_from_f(p.w, idx_f32(lb + (double)(j + 2 * NT * u)))), s, c);
-#endif
+                rx_sincos(p, phase_from_f(p.w, idx_f32(lb + (double)(j + 2 * NT * u))), s, c);
                 float2 z;
                 if (MIX == MIX_REFERENCE_REAL) z = make_float2(x[j].x * c, x[j].x * -s);
                 else z = make_float2(__builtin_fmaf(x[j].y, s, x[j].x * c),
@@ -298,10 +301,6 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
 #pragma unroll
             for (int i = 0; i < R; ++i) win[i] = ldc(base + i);
             int k = 0;
-#ifdef MODEM_ABLATE_FIR
-            k = K;
-            acc[0] += win[0];
-#endif
             for (; k + CH <= K; k += CH) {
                 const float2* pc = base - (k + CH);   // positive ds_read immediates
 #pragma unroll
@@ -335,19 +334,13 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
 // Every real operand is split in two f16 halves, a = a_hi + a_lo (round to nearest), and
 //   A*B ~= A_hi*B_hi + A_hi*B_lo + A_lo*B_hi      (dropped A_lo*B_lo < 2^-22 |a||b|)
 // accumulates in f32: 6 MFMAs (re and im rails) per 32-sample k-step, 16x the MAC rate of
-// the f32 MFMA. Range: the taps are scaled by 2^kb on the host (0 when their max is in [2^-3, 2^15)); the
-// mixed samples of a tile are used as they are when the tile's max |z| lies in
-// [2^-3, 2^15) (results then never depend on how a stream is cut into calls), and scaled
-// by 2^ka into [2^14, 2^15) otherwise. Outputs are scaled back with ldexp (exact).
-// LDS: four f16 planes (re_hi, re_lo, im_hi, im_lo) in natural sample order with 16 pad
-// halves after every RW = 16*DEC samples (rxh_pos: conflict-free 16-B A reads), and NC shifted copies of the hi/lo reversed-tap table so that every lane's
-// 8-tap B read is one aligned ds_read_b128.
-template <int DEC, int NT_> struct RxMfmaCfg {
-    static constexpr int NT = NT_;               // 64 (one wave) or 256 (4 waves)
-    static constexpr int TS = NT / 64 * 256;     // kept instants per workgroup tile
-    static constexpr int RW = 16 * DEC;          // samples per A row
-    static constexpr int RP = RW + 16;           // padded row pitch (halves)
-};
+// the f32 MFMA. Range: the taps are scaled by 2^kb on the host (0 when their max is in
+// [2^-3, 2^15)); the mixed samples of a tile by 2^ka, ka = tile_ka of the tile's max |z| (0
+// inside [2^-3, 2^15), so results never depend on how a stream is cut into calls). Outputs
+// are scaled back with ldexp (exact).
+// LDS: four f16 planes (re_hi, re_lo, im_hi, im_lo) and NC shifted copies of the hi/lo
+// reversed-tap table, so that every lane's 8-tap B read is one aligned ds_read_b128.
+
 // Plane position of staged sample e: 16 pad halves after every RW samples. With the row pitch
 // RW + 16 (= 2 mod 4 in 16-B units), the 16 lanes of each ds_read_b128 lane group (rows i at
 // k-offset g, rows i' at g + 1) hit distinct bank quads; a pitch of RW + 8 was 2-way conflicted.
@@ -357,61 +350,33 @@ __host__ __device__ constexpr int rxh_pos(int e, int RW) { return e + 16 * (e / 
 // (RXE_GEN: any other combination, guarded per store).
 enum { RXE_GEN = 0, RXE_IQ = 1, RXE_SYM = 2, RXE_IQSYM = 3, RXE_NEAREST = 4 };   // | NEAREST: LUT slicer
 
-__device__ __forceinline__ uint8_t rx_slice_qam(const RxParams& p, float re, float im) {
-#pragma clang fp contract(off)
-    const int ms = (int)p.max_symbol;
-    const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
-    const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
-    // clamp before the conversion: huge / NaN inputs stay defined (fmax drops a NaN)
-    const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), (float)ms);
-    const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), (float)ms);
-    return (uint8_t)((si << p.bits_per_carrier) | sq);
-}
-
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-// hi = rn_f16(v), lo = rn_f16(v - hi) for two values (v - hi is exact in f32).
+// hi = rn_f16(v), lo = rn_f16(v - hi) for two values: one v_cvt_pk_f16_f32 and two
+// v_fma_mix{lo,hi}_f16 that round the exact f32 remainder v - hi straight into the packed
+// lo halves (3 VALU per pair).
 __device__ __forceinline__ void split2(cf2 v, h2& hi, h2& lo) {
     hi = __builtin_convertvector(v, h2);
-    float l0, l1;                                   // v - hi, exact: one v_fma_mix_f32 each
-    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l0) : "v"(hi), "v"(v.x));
-    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(l1) : "v"(hi), "v"(v.y));
-    lo = __builtin_convertvector((cf2){l0, l1}, h2);
+    uint32_t l;
+    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hi), "v"(v.x));
+    asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hi), "v"(v.y));
+    lo = __builtin_bit_cast(h2, l);
 }
 
 // Conjugate mix of one sample, packed: (re, im) = (x*cs + y*sn, y*cs - x*sn) with the same
-// roundings as fma(y, sn, x*cs) / fma(-x, sn, y*cs). cssn = (cs, sn). Written as vector ops
-// (v_pk_mul_f32 + v_pk_fma_f32 with op_sel / neg modifiers), so that the compiler's hazard
-// recognizer sees them and only pads where a transcendental's result is read too early.
+// roundings as fma(y, sn, x*cs) / fma(-x, sn, y*cs). cssn = (cs, sn).
 __device__ __forceinline__ cf2 cmix(cf2 x, cf2 cssn) {
-#ifdef MODEM_CMIX_ASM
-    cf2 t, z;
-    asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(x), "v"(cssn));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
-        : "=v"(z) : "v"(x), "v"(cssn), "v"(t));
-    return z;
-#else
     const cf2 t = x * cssn.xx;
     return __builtin_elementwise_fma(x.yx, (cf2){cssn.y, -cssn.y}, t);
-#endif
 }
 
 // Four consecutive input samples (one lane's staging quad).
 template <typename InT> struct Quad;
 template <> struct Quad<float> {
     struct T { float4 a, b; };
-    __device__ static T load(const void* x, int64_t q) {      // q: sample index (8-B aligned)
-        const float4* v = reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(x) + q);
-#ifdef MODEM_RX_NT_LOAD
-        const f32x4* w = reinterpret_cast<const f32x4*>(v);
-        const f32x4 a = __builtin_nontemporal_load(w), b = __builtin_nontemporal_load(w + 1);
-        return T{make_float4(a[0], a[1], a[2], a[3]), make_float4(b[0], b[1], b[2], b[3])};
-#else
-        return T{v[0], v[1]};
-#endif
-    }
     __device__ static void split(const T& t, float2 (&x)[4]) {
         x[0] = make_float2(t.a.x, t.a.y); x[1] = make_float2(t.a.z, t.a.w);
         x[2] = make_float2(t.b.x, t.b.y); x[3] = make_float2(t.b.z, t.b.w);
@@ -419,9 +384,6 @@ template <> struct Quad<float> {
 };
 template <> struct Quad<__half> {
     using T = uint4;
-    __device__ static T load(const void* x, int64_t q) {
-        return *reinterpret_cast<const uint4*>(reinterpret_cast<const __half2*>(x) + q);
-    }
     __device__ static void split(const T& t, float2 (&x)[4]) {
         x[0] = __half22float2(*reinterpret_cast<const __half2*>(&t.x));
         x[1] = __half22float2(*reinterpret_cast<const __half2*>(&t.y));
@@ -436,60 +398,84 @@ __device__ __forceinline__ float wave_max(float m) {
     return m;
 }
 
-// Tile scale exponent from the lanes' max |z| (one barrier; red: 4 floats of LDS).
-template <int NT>
-__device__ __forceinline__ int tile_scale_exp(float lane_max, float* red) {
-    float m = wave_max(lane_max);
-    if (NT == 64) {
-        __syncthreads();                                    // one wave: orders the LDS planes only
-    } else {
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-        __syncthreads();
-        m = __builtin_fmaxf(__builtin_fmaxf(red[0], red[1]), __builtin_fmaxf(red[2], red[3]));
-    }
-    const int ex = (int)((__float_as_uint(m) >> 23) & 0xff);
-    if (ex >= 127 - 3 && ex < 127 + 15) return 0;          // max in [2^-3, 2^15): as is
-    if (ex == 0 || ex == 0xff) return 0;                    // all zero / non-finite
-    return 141 - ex;                                        // max * 2^k in [2^14, 2^15)
+// A tile's scale exponent ka as a function of the biased f32 exponent `ex` of its max |z|
+// (the split-f16 window): 0 when the max lies in [2^-3, 2^15) (or is zero / subnormal /
+// non-finite); otherwise the multiple of 8 that moves it into [2^-3, 2^5) (small tiles) or
+// [2^7, 2^15) (large ones). A pure function of the tile's content, so the fast path (which
+// stages with a predicted ka and keeps the tile only if the prediction equals this) and the
+// general path give identical results; steps of 8 binades keep the prediction from the
+// previous tile right for any slowly varying amplitude.
+__device__ __forceinline__ int tile_ka(int ex) {
+    if (ex <= 0 || ex >= 0xff || (ex >= 127 - 3 && ex < 127 + 15)) return 0;
+    const int k = ex < 127 - 3 ? 8 * ((127 - 3 - ex + 7) / 8) : -8 * ((ex - (127 + 14) + 7) / 8);
+    return k > 120 ? 120 : k;                                // 2^k stays a normal f32
 }
+__device__ __forceinline__ int f32_exp(float m) { return (int)((__float_as_uint(m) >> 23) & 0xff); }
 
 // The tiles one workgroup runs, in order: first, first + step, ... (count of them).
 struct TileSeq { int64_t first, step, count; };
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NTT>
+// Buffer descriptor over `bytes` bytes at `base` (wave-uniform inputs made provably uniform).
+// Accesses past `bytes` load zeros / are dropped without touching memory.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// QAM-axis decisions for (re, im) at once (rx_slice's roundings, contract off), the scale and
+// offset on the packed pipe.
+__device__ __forceinline__ uint8_t rx_slice_qam2(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    const cf2 f = ((cf2){re, im} * p.inv_scale + p.max_symbol) * 0.5f;
+    const float ms = p.max_symbol;
+    const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(f.x), 0.f), ms);
+    const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(f.y), 0.f), ms);
+    return (uint8_t)((si << p.bits_per_carrier) | sq);
+}
+
+// One workgroup of 4 waves per tile of TS = 1024 kept instants (persistent: XCD-matched
+// top-down rounds of tiles). Per tile the waves mix, scale and split the tile's input into the
+// LDS planes, reloading every staging slot with the next tile's samples as soon as it is
+// consumed (those loads are in flight through the rest of the staging, the matched filter
+// and the stores), then run the matched filter (16 rows of 16 instants per wave) and store
+// the outputs. Per staged sample the VALU does: the carrier index as one exact f32 add
+// (idx_split), the bit-exact phase (phase_from_f2), the turns and v_sin/v_cos, the packed
+// conjugate mix, an optional exact power-of-two scale, one v_max3 and the split.
+//
+// The f16 range: a tile is staged with a predicted tile_ka (the previous tile's; a call's
+// first from where the previous call ended, a stream's first from its raw input) and each
+// wave votes with three ballots whether the tile's max lies in that exponent's window. A tile
+// outside it, and the call's first tile (its window reads the history), take the general
+// path: per-sample loads, two passes, the same tile_ka -> identical results either way.
+template <int DEC, int NKS, typename InT, int MIX, typename OutT>
 struct RxMfma {
-    using C = RxMfmaCfg<DEC, NTT>;
     using Q = Quad<InT>;
     using QT = typename Q::T;
-    static constexpr int NT = C::NT, TS = C::TS, RW = C::RW, RP = C::RP;
+    static constexpr int NT = 256;                              // 4 waves
+    static constexpr int TS = 1024;                             // kept instants per tile
+    static constexpr int RW = 16 * DEC;                         // samples per A row
     static constexpr int W = 32 * NKS;
     static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
     static constexpr int NQ = (NS + 3) / 4;                     // quads
     static constexpr int U = (NQ + NT - 1) / NT;                // quads per lane
-    // Plane layout. decim 4 (4 waves): unpadded, 16-B chunks XOR-swizzled within each aligned
-    // group of 8 chunks — conflict-free A reads (tests/test_lds_banks.py) and 4 KiB less LDS
-    // per workgroup than padding, which lets 4 workgroups share a CU. Otherwise rxh_pos.
-#ifdef MODEM_RX_NOSWZ
-    static constexpr bool SWZ = false;
-#else
-    static constexpr bool SWZ = DEC == 4 && NT == 256;
-#endif
-    __host__ __device__ static constexpr int ppos(int e) {    // plane position of staged sample e
+    // Plane layout. decim 4: unpadded, 16-B chunks XOR-swizzled within each aligned group of
+    // 8 chunks — conflict-free A reads (tests/test_lds_banks.py) and 4 KiB less LDS per
+    // workgroup than padding, which lets 4 workgroups share a CU. Otherwise rxh_pos.
+    static constexpr bool SWZ = DEC == 4;
+    __host__ __device__ static constexpr int ppos(int e) {
         return SWZ ? ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7)) : rxh_pos(e, RW);
     }
     static constexpr int PL = SWZ ? (4 * NQ + 63) & ~63 : (rxh_pos(4 * NQ - 1, RW) + 1 + 7) & ~7;   // halves per plane
     static constexpr int NC = rx_mfma_table_copies(DEC);
     static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
-    static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 16;   // + red
+    static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 8 * 4;   // + votes, maxima
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
-    // Waves per SIMD the registers are held to: 4 for the swizzled layout (its LDS lets 4
-    // workgroups share a CU; the matched filter then single-buffers its operands to fit 128
-    // VGPRs: 35.0 vs 35.4 us on C3), else the compiler's choice (3 on C3).
-#ifdef MODEM_RX_NOWPE
-    static constexpr int WPE = 1;
-#else
+    // Waves per SIMD the registers are held to: 4 where the LDS lets 4 workgroups share a CU
+    // (the matched filter then single-buffers its operands to fit 128 VGPRs), else the
+    // compiler's choice.
     static constexpr int WPE = SWZ && LDS_BYTES <= 40960 ? 4 : 1;
-#endif
     static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
     // plane offset between staging slots (the swizzle repeats every 1024 samples)
     static constexpr int SLOT_POS = SWZ ? 4 * NT : 4 * NT + 16 * (4 * NT / RW);
@@ -497,172 +483,106 @@ struct RxMfma {
     // Rows hold 16 instants aligned to the absolute instant index (k % 16 == column), so an
     // instant's taps always fall at the same k positions of the 32-wide MFMA sums and the
     // result never depends on where a call starts. Tile t covers instants
-    // kb + t*TS .., kb = k_first - lead; outputs before k_first are computed and dropped.
+    // k_first - lead + t*TS ..; outputs before k_first are computed and dropped.
     __device__ static int lead(const RxParams& p) { return (int)(p.k_first & 15); }
     __device__ static int64_t q_lo_of(const RxParams& p, int64_t t) {
         return (p.k_first - lead(p) + t * TS) * DEC + p.D + 15 * DEC - W + 1 - p.n_start;
     }
 
-    // Scale, split and write samples e0..e0+3 at plane offset o = rxh_pos(e0) (e0 % 4 == 0:
-    // one row, 8-B aligned).
-    __device__ static void put4o(_Float16* pl, int o, const float (&zr)[4], const float (&zi)[4], float sc) {
-        h2 rh0, rl0, rh1, rl1, ih0, il0, ih1, il1;
-        split2((cf2){zr[0], zr[1]} * sc, rh0, rl0);
-        split2((cf2){zr[2], zr[3]} * sc, rh1, rl1);
-        split2((cf2){zi[0], zi[1]} * sc, ih0, il0);
-        split2((cf2){zi[2], zi[3]} * sc, ih1, il1);
-        *reinterpret_cast<h4*>(pl + o) = (h4){rh0.x, rh0.y, rh1.x, rh1.y};
-        *reinterpret_cast<h4*>(pl + PL + o) = (h4){rl0.x, rl0.y, rl1.x, rl1.y};
-        *reinterpret_cast<h4*>(pl + 2 * PL + o) = (h4){ih0.x, ih0.y, ih1.x, ih1.y};
-        *reinterpret_cast<h4*>(pl + 3 * PL + o) = (h4){il0.x, il0.y, il1.x, il1.y};
+    // threadIdx.x as a value the compiler cannot hoist: every lane-dependent quantity is then
+    // computed where it is used instead of once at the kernel entry, where kept live across
+    // the tile loop it would spill (a kernel with scratch runs fewer waves per CU: 38 vs
+    // 32.6 us on C3)
+    __device__ static int tid_() {
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        return t;
     }
 
-    // Steady state: the tile's samples lie inside the chunk, carrier index < 2^53. Staged
-    // at scale 1 (the tile max is tracked on the way). Returns the tile's scale exponent: 0,
-    // or for a tile whose max falls outside [2^-3, 2^15) the exponent the general path
-    // (stage_slow) must restage it with.
-    // Load staging slot u of the tile whose window starts at chunk sample `base` (clamped
-    // into the chunk by the caller); l0 = 4 * lane, opaque.
-    __device__ static QT load_slot(const RxParams& p, int64_t base, int l0, int u) {
-        int e0 = l0 + 4 * NT * u;
-        if ((u + 1) * NT > NQ) e0 = e0 < 4 * (NQ - 1) ? e0 : 4 * (NQ - 1);   // spare lanes
-#ifdef MODEM_ABLATE_LOAD
-        float v = 0.5f + 1e-3f * (float)(e0 & 7);   // in the f16 window: no restaging
-        asm volatile("" : "+v"(v));
-        if constexpr (std::is_same<InT, float>::value) return QT{make_float4(v, v, v, v), make_float4(v, v, v, v)};
-        else return make_uint4(__float_as_uint(v), 0, 0, 0);
-#else
-        return Q::load(p.x, base + e0);
-#endif
+    // Carrier index n_base + e as f32 for the staged samples e of a tile: n_base = A + b with A
+    // a multiple of 2^s exactly representable in f32 (s from the tile's largest index) and b
+    // < 2^22, so fl(A + (b + e)) — one f32 add of two exact values — is the correctly rounded
+    // `n as f32` (needs every index < 2^46: RxParams::idx46, checked on the host).
+    struct Idx { float a, bl; };
+    __device__ static Idx idx_split(uint64_t n_base) {
+        const uint64_t n_max = n_base + NS;
+        const int e = 63 - __builtin_clzll(n_max | 1);
+        const int sh = e > 23 ? e - 23 : 0;
+        const uint64_t A = n_base & ~((1ull << sh) - 1);
+        const float af = __builtin_ldexpf((float)(uint32_t)(A >> sh), sh);      // exact
+        const uint32_t b = (uint32_t)(n_base - A) + 4u * (uint32_t)tid_();
+        return Idx{__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, af))),
+                   (float)b};
     }
 
-    // Steady-state staging of one tile from the prefetched registers `pre`. (Reloading each
-    // slot for the next tile right after it is consumed, to give the loads a whole tile period,
-    // measured 1 us slower on C3 than prefetching after the stage.)
-    __device__ static int stage_fast(const RxParams& p, _Float16* pl, float* red, double nbd,
-                                     const QT (&pre)[U]) {
-        const int tid = threadIdx.x;
-        // carrier index of the lane's first sample; opaque, so that the per-sample offsets
-        // stay immediates instead of 4*U hoisted loop-invariant VGPRs
-        double lb = nbd + (double)(4 * tid);
-        int pos0 = ppos(4 * tid);                         // slot u writes at pos0 + u * SLOT_POS
-        asm volatile("" : "+v"(lb), "+v"(pos0));
-        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        float mx = 0.f;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            // the last slot is partial: only the waves that own some of its quads run it
-            if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) continue;   // wave-uniform
-            float2 x[4];
-            Q::split(pre[u], x);
-            const int e0 = 4 * (tid + NT * u);
-            float zr[4], zi[4];
-            // the quad's phases as two packed pairs, computed side by side (independent
-            // chains fill each other's VALU dependency wait states)
-            cf2 sn2[2], cs2[2];
-            {
-                const cf2 nf0 = (cf2){idx_f32(lb + (double)(4 * NT * u)), idx_f32(lb + (double)(4 * NT * u + 1))};
-                const cf2 nf1 = (cf2){idx_f32(lb + (double)(4 * NT * u + 2)), idx_f32(lb + (double)(4 * NT * u + 3))};
-#ifdef MODEM_ABLATE_MIX
-                sn2[0] = sn2[1] = (cf2){0.f, 0.f}; cs2[0] = nf0; cs2[1] = nf1;
-#else
-                // rx_phase: one add on the packed phases (no product to contract)
-                const cf2 ph0 = phase_from_f2(p.w, nf0) + p.phase_offset;
-                const cf2 ph1 = phase_from_f2(p.w, nf1) + p.phase_offset;
-                sincos_phase2(ph0, sn2[0], cs2[0]);
-                sincos_phase2(ph1, sn2[1], cs2[1]);
-#endif
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j += 2) {
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const float sn = sn2[j / 2][i], cs = cs2[j / 2][i];
-                    if (MIX == MIX_REFERENCE_REAL) { zr[j + i] = x[j + i].x * cs; zi[j + i] = x[j + i].x * -sn; }
-                    else {
-                        const cf2 z = cmix((cf2){x[j + i].x, x[j + i].y}, (cf2){cs, sn});
-                        zr[j + i] = z.x; zi[j + i] = z.y;
-                    }
-                    // only the last slot can reach past the tile: its extra samples are not counted
-                    if ((u + 1) * 4 * NT <= NS || e0 + j + i < NS)      // one v_max3 per sample
-                        asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j + i]), "v"(zi[j + i]));
-                }
-            }
-#ifdef MODEM_ABLATE_PUT
-            asm volatile("" :: "v"(zr[0]), "v"(zr[1]), "v"(zr[2]), "v"(zr[3]), "v"(zi[0]), "v"(zi[1]), "v"(zi[2]), "v"(zi[3]));
-#else
-            if ((u + 1) * 4 * NT <= NS || e0 < NS) put4o(pl, pos0 + u * SLOT_POS, zr, zi, 1.0f);
-#endif
-            __builtin_amdgcn_sched_barrier(0);              // one quad's temporaries at a time
+    // Window of a tile staged with exponent k (see tile_ka): [lo, hi) for its max |z|.
+    __device__ static cf2 window(int k) {
+        return k == 0 ? (cf2){0x1p-3f, 0x1p15f} : k > 0 ? (cf2){0x1p-3f, 0x1p5f} : (cf2){0x1p7f, 0x1p15f};
+    }
+    // After the barrier: do the waves' votes put the staged tile inside the window of k?
+    // (k == 0 also accepts an all-zero / subnormal tile, whose tile_ka is 0.)
+    __device__ static bool fast_ok(const int* votes, int k) {
+        const int f = votes[0] | votes[1] | votes[2] | votes[3];
+        const bool good = k == 0 ? !(f & 2) && ((f & 1) || !(f & 4)) : (f & 1) && !(f & 2);
+        return __builtin_amdgcn_readfirstlane((int)good) != 0;
+    }
+    __device__ static int read_ka(const float* r) {
+        return __builtin_amdgcn_readfirstlane(tile_ka(f32_exp(
+            __builtin_fmaxf(__builtin_fmaxf(r[0], r[1]), __builtin_fmaxf(r[2], r[3])))));
+    }
+
+    // Staging slot u of a tile through a buffer descriptor whose base is the tile window's
+    // first sample and whose size is what of its 4 * NQ samples lies in the chunk (0 bytes: no
+    // next tile). Loads past the size return zeros without touching memory (the spare lanes of
+    // the last slot; a call's last tile; a workgroup's last tile), so the reload of every slot
+    // is unconditional.
+    __device__ static __amdgpu_buffer_rsrc_t window_rsrc(const RxParams& p, int64_t q_lo, bool live) {
+        constexpr int S = sizeof(InT) * 2;
+        const int64_t avail = p.N - q_lo;
+        const uint32_t w = avail < 4 * NQ ? (uint32_t)(avail > 0 ? avail : 0) : (uint32_t)(4 * NQ);
+        return buf_rsrc(reinterpret_cast<const char*>(p.x) + q_lo * S, live ? w * (uint32_t)S : 0u);
+    }
+    __device__ static QT load_slot(__amdgpu_buffer_rsrc_t r, int voff, int u) {
+        constexpr int S = sizeof(InT) * 2;
+        const int o = voff + 4 * NT * u * S;
+        if constexpr (std::is_same<InT, float>::value) {
+            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, 0));
+            return QT{make_float4(a[0], a[1], a[2], a[3]), make_float4(b[0], b[1], b[2], b[3])};
+        } else {
+            return __builtin_bit_cast(QT, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
         }
-        // ka != 0 (rare: out-of-window magnitudes): the caller restages the tile scaled
-#ifdef MODEM_ABLATE_TMAX
-        asm volatile("" :: "v"(mx));
-        __syncthreads();
-        return 0;
-#endif
-        return tile_scale_exp<NT>(mx, red);
     }
 
-    // First / last tiles of a chunk, unaligned input, carrier index >= 2^53: per sample, two
-    // passes (max, then scale + split).
-    __device__ static int stage_slow(const RxParams& p, _Float16* pl, float* red, int64_t q_lo) {
-        const int64_t n_lo = q_lo + p.n_start;
-        float mx = 0.f;
-        for (int e0 = 4 * threadIdx.x; e0 < NS; e0 += 4 * NT)
-            for (int j = 0; j < 4 && e0 + j < NS; ++j) {
-                const float2 z = rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j));
-                mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(z.x), __builtin_fabsf(z.y)));
-            }
-        const int ka = tile_scale_exp<NT>(mx, red);
-        const float sc = __builtin_ldexpf(1.0f, ka < -126 ? -126 : (ka > 127 ? 127 : ka));
-        for (int e0 = 4 * threadIdx.x; e0 < NS; e0 += 4 * NT) {
-            float zr[4], zi[4];
-            for (int j = 0; j < 4; ++j) {
-                const float2 z = e0 + j < NS ? rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j))
-                                             : make_float2(0.f, 0.f);
-                zr[j] = z.x; zi[j] = z.y;
-            }
-            put4o(pl, ppos(e0), zr, zi, sc);
-        }
-        return ka;
-    }
-
-    // One 16x16 tile per wave. Lane (i = lane & 15, g = lane >> 4) reads A row i, samples
-    // 32s + 8g .. +7, and B[32s + 8g + j][c = i] = T[32s + 8g + j + (15 - c)*DEC].
+    // One 16x16 output block per wave: rows 16 wave .. 16 wave + 15 of the tile. Lane
+    // (i = lane & 15, g = lane >> 4) reads A row i, samples 32s + 8g .. +7, and
+    // B[32s + 8g + j][c = i] = T[32s + 8g + j + (15 - c)*DEC] from the table copy that makes
+    // the read aligned. WPE 4: one k-step's operands at a time (fewer registers; the other
+    // waves hide the LDS latency); otherwise the next k-step's load during this one's MFMAs.
     __device__ static void fir(const _Float16* pl, const _Float16* tbl, f32x4& dre, f32x4& dim) {
-        const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        constexpr bool DB = WPE < 4;
+        const int lane = tid_() & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         const int i = lane & 15, g = lane >> 4;
-        const _Float16* arow = pl + (16 * wave + i) * RP + 8 * g;
-        const int ae = (16 * wave + i) * RW + 8 * g;            // sample of this lane's first A read
-        const int xb = 8 * g + (15 - i) * DEC;                  // B start for this lane's column
-        const int q = xb & 7;                                   // copy with Tq[y] = T[y + q]
+        const int ae = (16 * wave + i) * RW + 8 * g;
+        const int xb = 8 * g + (15 - i) * DEC;
+        const int q = xb & 7;
         const _Float16* brow = tbl + (q / (8 / NC)) * 2 * TB + (xb - q);
-#ifdef MODEM_ABLATE_FIR
-        const h8 a0 = *reinterpret_cast<const h8*>(arow);
-        dre = (f32x4){(float)a0[0], 0.f, 0.f, 0.f};
-        dim = (f32x4){(float)brow[0], 0.f, 0.f, 0.f};
-        return;
-#endif
-        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;     // one accumulator per rail
-        auto aoff = [](int s) { return 32 * s + 16 * ((32 * s) / RW); };
+        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;
         h8 a[2][4], b[2][2];
-        auto load = [&](int s, int slot) {
-            const _Float16* ap = SWZ ? pl + ppos(ae + 32 * s) : arow + aoff(s);
-            a[slot][0] = *reinterpret_cast<const h8*>(ap);
-            a[slot][1] = *reinterpret_cast<const h8*>(ap + PL);
-            a[slot][2] = *reinterpret_cast<const h8*>(ap + 2 * PL);
-            a[slot][3] = *reinterpret_cast<const h8*>(ap + 3 * PL);
-            b[slot][0] = *reinterpret_cast<const h8*>(brow + 32 * s);
-            b[slot][1] = *reinterpret_cast<const h8*>(brow + TB + 32 * s);
+        auto load = [&](int s, int c) {
+            const _Float16* ap = pl + ppos(ae + 32 * s);
+            a[c][0] = *reinterpret_cast<const h8*>(ap);
+            a[c][1] = *reinterpret_cast<const h8*>(ap + PL);
+            a[c][2] = *reinterpret_cast<const h8*>(ap + 2 * PL);
+            a[c][3] = *reinterpret_cast<const h8*>(ap + 3 * PL);
+            b[c][0] = *reinterpret_cast<const h8*>(brow + 32 * s);
+            b[c][1] = *reinterpret_cast<const h8*>(brow + TB + 32 * s);
         };
-        // WPE 4: single-buffered operands (fewer registers; the other waves hide the LDS
-        // latency); otherwise the next k-step's operands load during this one's products
-        if (WPE < 4) load(0, 0);
+        if (DB) load(0, 0);
 #pragma unroll
         for (int s = 0; s < NKS; ++s) {
-            const int c = WPE < 4 ? s & 1 : 0;
-            if (WPE >= 4) load(s, 0);
+            const int c = DB ? s & 1 : 0;
+            if (!DB) load(s, 0);
             else if (s + 1 < NKS) load(s + 1, c ^ 1);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][0], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
@@ -676,135 +596,258 @@ struct RxMfma {
         dim = m0;
     }
 
-    // D[row][col]: row = 4*(lane>>4) + r, col = lane&15 -> instant ot + 16*row + col.
-    template <int EM>
-    __device__ static void emit_full(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
-        const int lane = threadIdx.x & 63;
-#ifdef MODEM_ABLATE_STORE
+    // Split z (4 samples) and write it at plane offset o.
+    __device__ static void put4(_Float16* pl, int o, const float (&zr)[4], const float (&zi)[4]) {
+        h2 rh0, rl0, rh1, rl1, ih0, il0, ih1, il1;
+        split2((cf2){zr[0], zr[1]}, rh0, rl0);
+        split2((cf2){zr[2], zr[3]}, rh1, rl1);
+        split2((cf2){zi[0], zi[1]}, ih0, il0);
+        split2((cf2){zi[2], zi[3]}, ih1, il1);
+        *reinterpret_cast<h4*>(pl + o) = (h4){rh0.x, rh0.y, rh1.x, rh1.y};
+        *reinterpret_cast<h4*>(pl + PL + o) = (h4){rl0.x, rl0.y, rl1.x, rl1.y};
+        *reinterpret_cast<h4*>(pl + 2 * PL + o) = (h4){ih0.x, ih0.y, ih1.x, ih1.y};
+        *reinterpret_cast<h4*>(pl + 3 * PL + o) = (h4){il0.x, il0.y, il1.x, il1.y};
+    }
+
+    // Fast-path staging of one tile from the prefetched registers `pre` at scale 2^k (SC:
+    // k != 0; sc = 2^k, win = window(k)), reloading each slot with the next tile's samples
+    // (`nxt`). Each wave writes its three votes (max >= window lo, >= window hi, normal).
+    template <bool SC>
+    __device__ static void stage(const RxParams& p, _Float16* pl, int* vote, Idx ix, float sc, cf2 win,
+                                 QT (&pre)[U], __amdgpu_buffer_rsrc_t nxt) {
+        const int tid = tid_();
+        int pos0 = ppos(4 * tid);
+        int voff = 4 * tid * (int)sizeof(InT) * 2;
+        float bl = ix.bl;
+        asm volatile("" : "+v"(pos0), "+v"(voff), "+v"(bl));
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const float roff = p.phase_offset * kRcp2Pi;          // rx_sincos: carrier + PLL offset, in turns
+        float mx = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(dre[r]), "v"(dim[r]));
-        return;
-#endif
-        // uniform base pointers + 32-bit lane offsets: saddr + voffset stores, no 64-bit
-        // per-lane address registers
-        OutT* qb = reinterpret_cast<OutT*>(p.out_iq) + 2 * ot;
-        uint8_t* sb = p.out_sym + ot;
+        for (int u = 0; u < U; ++u) {
+            if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) {   // partial last slot: not this wave's
+                pre[u] = load_slot(nxt, voff, u);
+                continue;
+            }
+            float2 x[4];
+            Q::split(pre[u], x);
+            const int e0 = 4 * (tid + NT * u);
+            const float bu = bl + (float)(4 * NT * u);
+            const cf2 nf0 = (bu + (cf2){0.f, 1.f}) + ix.a;            // exact, then one rounding
+            const cf2 nf1 = (bu + (cf2){2.f, 3.f}) + ix.a;
+            const cf2 rv0 = __builtin_elementwise_fma(phase_from_f2(p.w, nf0), (cf2){kRcp2Pi, kRcp2Pi}, (cf2){roff, roff});
+            const cf2 rv1 = __builtin_elementwise_fma(phase_from_f2(p.w, nf1), (cf2){kRcp2Pi, kRcp2Pi}, (cf2){roff, roff});
+            const cf2 sn2[2] = {(cf2){__builtin_amdgcn_sinf(rv0.x), __builtin_amdgcn_sinf(rv0.y)},
+                                (cf2){__builtin_amdgcn_sinf(rv1.x), __builtin_amdgcn_sinf(rv1.y)}};
+            const cf2 cs2[2] = {(cf2){__builtin_amdgcn_cosf(rv0.x), __builtin_amdgcn_cosf(rv0.y)},
+                                (cf2){__builtin_amdgcn_cosf(rv1.x), __builtin_amdgcn_cosf(rv1.y)}};
+            float zr[4], zi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float sn = sn2[j / 2][j % 2], cs = cs2[j / 2][j % 2];
+                cf2 z;
+                if (MIX == MIX_REFERENCE_REAL) z = (cf2){x[j].x * cs, x[j].x * -sn};
+                else z = cmix((cf2){x[j].x, x[j].y}, (cf2){cs, sn});
+                if (SC) z = z * sc;
+                zr[j] = z.x;
+                zi[j] = z.y;
+                // only the last slot can reach past the tile: its extra samples are not counted
+                if ((u + 1) * 4 * NT <= NS || e0 + j < NS)
+                    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j]), "v"(zi[j]));
+            }
+            if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, pos0 + u * SLOT_POS, zr, zi);
+            pre[u] = load_slot(nxt, voff, u);                  // the next tile's slot u, same registers
+            __builtin_amdgcn_sched_barrier(0);                 // one quad's temporaries at a time
+        }
+        // three votes per wave instead of a max reduction
+        const bool blo = __ballot(mx >= win.x) != 0, bhi = __ballot(mx >= win.y) != 0,
+                   bn = __ballot(mx >= 0x1p-126f) != 0;
+        if ((tid & 63) == 0) vote[wave] = (blo ? 1 : 0) | (bhi ? 2 : 0) | (bn ? 4 : 0);
+    }
+
+    // D[row][col]: row = 4*(lane>>4) + r, col = lane&15 -> instant ot + 16*row + col. Stores
+    // through buffer descriptors sized to the instants still in the call (a call's last tile
+    // computes past them).
+    template <int EM>
+    __device__ static void emit(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
+        const int lane = tid_() & 63;
+        if (EM == RXE_GEN) {                   // any other output combination: guarded stores
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t o = ot + 16 * (4 * (lane >> 4) + r) + (lane & 15);
+                if (o < p.nout)
+                    rx_emit<OutT>(p, o, GAIN * __builtin_ldexpf(dre[r], -kab), GAIN * __builtin_ldexpf(dim[r], -kab));
+            }
+            return;
+        }
+        const int64_t left = p.nout - ot;
+        const uint32_t nk = left < 256 ? (uint32_t)(left > 0 ? left : 0) : 256u;
+        const __amdgpu_buffer_rsrc_t riq = buf_rsrc(reinterpret_cast<OutT*>(p.out_iq) + 2 * ot, nk * 2 * sizeof(OutT));
+        const __amdgpu_buffer_rsrc_t rsy = buf_rsrc(p.out_sym + ot, nk);
+        f32x4 re = dre, im = dim;
+        if (kab != 0) {                        // uniform
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { re[r] = __builtin_ldexpf(re[r], -kab); im[r] = __builtin_ldexpf(im[r], -kab); }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const uint32_t off = (uint32_t)(16 * (4 * (lane >> 4) + r) + (lane & 15));
-            float re = dre[r], im = dim[r];
-            if (kab != 0) { re = __builtin_ldexpf(re, -kab); im = __builtin_ldexpf(im, -kab); }   // uniform
-            re *= GAIN;
-            im *= GAIN;
-            if (EM == RXE_GEN) {
-                rx_emit<OutT>(p, ot + off, re, im);
-                continue;
+            const float a = re[r] * GAIN, b = im[r] * GAIN;
+            if (EM & RXE_IQ) {
+                if constexpr (std::is_same<OutT, float>::value)
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(a, b)), riq, 8 * off, 0, 0);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, __floats2half2_rn(a, b)), riq, 4 * off, 0, 0);
             }
-            if (EM & RXE_IQ) OutIO<OutT>::store_one(qb, off, re, im);
-            if (EM & RXE_SYM)
-                sb[off] = !(EM & RXE_NEAREST) ? rx_slice_qam(p, re, im)
-                        : p.bps == 2 ? rx_slice_nearest4(p, re, im) : rx_slice_nearest(p, re, im);
+            if (EM & RXE_SYM) {
+                const uint8_t sy = !(EM & RXE_NEAREST) ? rx_slice_qam2(p, a, b)
+                                 : p.bps == 2 ? rx_slice_nearest4(p, a, b) : rx_slice_nearest(p, a, b);
+                __builtin_amdgcn_raw_buffer_store_b8(sy, rsy, off, 0, 0);
+            }
         }
     }
 
-    __device__ static void emit_edge(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
-        const int lane = threadIdx.x & 63;
+    // General path for tile t (all waves): two passes over its samples (max, then tile_ka
+    // scale + split), the matched filter, the outputs in range. Returns its tile_ka.
+    __device__ static int slow_tile(const RxParams& p, _Float16* pl, const _Float16* tbl, float* reds, int64_t t,
+                                    int kb, int ld) {
+        // lane values recomputed here, not hoisted to the kernel entry (where, live across
+        // the tile loop, they would spill)
+        const int tid = tid_();
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int64_t q_lo = q_lo_of(p, t), n_lo = q_lo + p.n_start;
+        float mx = 0.f;
+        for (int e0 = 4 * tid; e0 < NS; e0 += 4 * NT)
+            for (int j = 0; j < 4 && e0 + j < NS; ++j) {
+                const float2 z = rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j));
+                mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(z.x), __builtin_fabsf(z.y)));
+            }
+        mx = wave_max(mx);
+        if ((tid & 63) == 0) reds[wave] = mx;
+        __syncthreads();
+        const int ka = read_ka(reds);
+        const float sc = __builtin_ldexpf(1.0f, ka);
+        for (int e0 = 4 * tid; e0 < NS; e0 += 4 * NT) {
+            float zr[4], zi[4];
+            for (int j = 0; j < 4; ++j) {
+                const float2 z = e0 + j < NS ? rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j))
+                                             : make_float2(0.f, 0.f);
+                zr[j] = z.x * sc;
+                zi[j] = z.y * sc;
+            }
+            put4(pl, ppos(e0), zr, zi);
+        }
+        __syncthreads();
+        f32x4 dre, dim;
+        fir(pl, tbl, dre, dim);
+        const int64_t ot = t * TS + wave * 256 - ld;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int64_t o = ot + 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            const int64_t o = ot + 16 * (4 * ((tid & 63) >> 4) + r) + (tid & 15);
             if (o >= 0 && o < p.nout)
-                rx_emit<OutT>(p, o, GAIN * __builtin_ldexpf(dre[r], -kab), GAIN * __builtin_ldexpf(dim[r], -kab));
+                rx_emit<OutT>(p, o, GAIN * __builtin_ldexpf(dre[r], -(ka + kb)), GAIN * __builtin_ldexpf(dim[r], -(ka + kb)));
+        }
+        __syncthreads();                       // the planes are restaged next
+        return ka;
+    }
+
+    // A tile on the fast path: its window starts inside the chunk and its first instant is
+    // kept (samples past the chunk's end load as zeros and instants past the call's last are
+    // not stored, both through the buffer descriptors' bounds); the call's first tile, which
+    // reads the history, takes the general path. `fast`: 4-B aligned input, carrier indices
+    // < 2^46 (idx_split).
+    struct Ctx {
+        bool fast;
+        int kb, ld;
+        __device__ bool full(const RxParams& p, int64_t t) const {
+            return fast && q_lo_of(p, t) >= 0 && t * TS >= ld;
+        }
+    };
+
+    // Tiles i .. while their staging exponent keeps its class (SC: nonzero). Returns at the end
+    // of the sequence, or after the barrier of a tile the general path must redo.
+    template <bool SC, int EM>
+    __device__ static void loop(const RxParams& p, _Float16* pl, const _Float16* tbl, int* votes, const TileSeq sq,
+                                const Ctx& cx, QT (&pre)[U], int64_t& i, int kpred) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const float sc = __builtin_ldexpf(1.0f, kpred);
+        const cf2 win = window(kpred);
+        while (i < sq.count) {
+            const int64_t t = sq.first + i * sq.step;
+            const bool fi = cx.full(p, t);
+            const bool pf = i + 1 < sq.count && cx.full(p, t + sq.step);
+            const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? q_lo_of(p, t + sq.step) : 0, pf);
+            const Idx ix = idx_split(p.c0 + (uint64_t)(q_lo_of(p, t) + p.n_start));
+            stage<SC>(p, pl, votes, ix, sc, win, pre, nxt);
+            __syncthreads();
+            if (!(fi && fast_ok(votes, kpred))) return;
+            f32x4 dre, dim;
+            fir(pl, tbl, dre, dim);
+            emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
+            __syncthreads();                   // the planes are restaged next
+            ++i;
         }
     }
 
-    // The tiles of `sq` (the XCD-matched top-down rounds of rx_mfma_body; a contiguous range
-    // per workgroup measured 9 % faster on C3 than bottom-up rounds, and dynamic tile handout
-    // through per-XCD atomic counters did not beat it either). When the input is 8-B aligned
-    // and the carrier indices stay below 2^53, the run of "full" tiles (all staged samples
-    // inside the chunk, all 1024 instants kept) goes through the prefetched loop, whose
-    // epilogue EM stores unconditionally; the first and last tiles of the chunk take the
-    // general path.
     template <int EM>
-    __device__ static void run(const RxParams& p, _Float16* pl, const _Float16* tbl, float* red,
-                               const TileSeq sq) {
-        const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // scalar
-        // quad loads need dword alignment only (16-B loads at 8-B aligned sample offsets)
-        const bool fast = p.exact_idx && ((uintptr_t)p.x & 3) == 0;
-        const int kb = p.tap_scale_exp;
-        const int ld = lead(p);
-        auto full = [&](int64_t t) {
-            const int64_t q = q_lo_of(p, t);
-            return fast && q >= 0 && q + 4 * NQ <= p.N && t * TS >= ld && (t + 1) * TS - ld <= p.nout;
-        };
+    __device__ static void run(const RxParams& p, _Float16* pl, const _Float16* tbl, float* red, const TileSeq sq,
+                               int64_t bid) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
+        int* votes = reinterpret_cast<int*>(red);            // [4]
+        float* reds = red + 4;                               // [4]
         QT pre[U];
-        // Base clamped into the chunk; issued when this workgroup has a next tile (a non-full
-        // next tile is restaged). The epilogue's stores stay unconditional, so the next trip's
-        // vmcnt waits remain counted.
-        auto clamped_base = [&](int64_t t) {
-            const int64_t base = q_lo_of(p, t);   // (the first tile of a call may start before 0)
-            return base > p.N - 4 * NQ ? p.N - 4 * NQ : base < 0 ? 0 : base;
-        };
-        auto prefetch = [&](int64_t t) {
-            const int64_t base = clamped_base(t);
-            int l0 = 4 * tid;                               // opaque: no per-slot hoisted addresses
-            asm volatile("" : "+v"(l0));
+        auto prefetch = [&](int64_t t, bool live) {
+            const __amdgpu_buffer_rsrc_t r = window_rsrc(p, live ? q_lo_of(p, t) : 0, live);
+            const int voff = 4 * tid_() * (int)sizeof(InT) * 2;
 #pragma unroll
-            for (int u = 0; u < U; ++u)                     // the partial last slot: its waves only
-                if ((u + 1) * NT <= NQ || 64 * wave + NT * u < NQ) pre[u] = load_slot(p, base, l0, u);
+            for (int u = 0; u < U; ++u) pre[u] = load_slot(r, voff, u);
         };
-        int64_t i = 0, t = sq.first;
-        bool restage = false;
-        STAMP_DECL;
+        const bool f0 = cx.full(p, sq.first);
+        prefetch(sq.first, f0);
+        // the first prediction: where the previous call ended (any exponent tile_ka can give)
+        const int kin = *p.ka_in;
+        int kpred = kin >= -120 && kin <= 120 && (kin & 7) == 0 ? kin : 0;
+        if (f0 && kin == INT32_MIN) {          // a stream's first call: from the first tile's raw input
+            float mx = 0.f;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) continue;
+                float2 x[4];
+                Q::split(pre[u], x);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(x[j].x), "v"(x[j].y));
+            }
+            mx = wave_max(mx);
+            if ((tid_() & 63) == 0) reds[wave] = mx;
+            __syncthreads();
+            kpred = read_ka(reds);
+            __syncthreads();
+        }
+        int64_t i = 0;
         while (i < sq.count) {
-            if (full(t) && !restage) {
-                prefetch(t);
-                for (; i < sq.count && full(t); ++i, t += sq.step) {
-                    const int64_t n_lo = q_lo_of(p, t) + p.n_start;
-#ifdef MODEM_STAMPS
-                    STAMP(0);                              // loop overhead
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    STAMP(1);                              // waiting for the tile's samples
-#endif
-                    const int ka = stage_fast(p, pl, red, (double)(p.c0 + (uint64_t)n_lo), pre);
-                    STAMP(2);                              // staging + tile-max barrier
-                    if (ka != 0) { restage = true; break; }       // uniform; leaves the loop
-                    // (the tile-max reduction in stage_fast ended with a barrier: planes visible)
-                    if (i + 1 < sq.count) prefetch(t + sq.step);   // next samples fly during the MFMAs
-                    STAMP(3);                              // prefetch issue
-                    f32x4 dre, dim;
-                    fir(pl, tbl, dre, dim);
-                    STAMP(4);                              // matched filter
-                    emit_full<EM>(p, t * TS + wave * 256 - ld, dre, dim, kb);
-                    STAMP(5);                              // epilogue
-                    __syncthreads();                       // LDS is restaged next trip
-                    STAMP(6);                              // end barrier
-                }
-            } else {
-                __syncthreads();                           // `red` and the planes are reused
-                restage = false;
-                const int ka = stage_slow(p, pl, red, q_lo_of(p, t));
-                __syncthreads();
-                f32x4 dre, dim;
-                fir(pl, tbl, dre, dim);
-                emit_edge(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
-                __syncthreads();
+            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
+            else loop<true, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
+            if (i < sq.count) {                // tile i on the general path (one place in the code)
+                kpred = slow_tile(p, pl, tbl, reds, sq.first + i * sq.step, cx.kb, cx.ld);
                 ++i;
-                t += sq.step;
-                STAMP(7);                                  // general-path tiles
+                // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
+                // not held across the general path, which has no registers to spare)
+                const int64_t t = sq.first + i * sq.step;
+                prefetch(t, i < sq.count && cx.full(p, t));
             }
         }
-        STAMP_FLUSH(blockIdx.x * (NT / 64) + wave);
+        if (bid == 0 && threadIdx.x == 0) *p.ka_out = kpred;   // the next call's first prediction
     }
-
 };
 
-// (Capping this kernel at 4 waves/SIMD fits the steady loop in 128 registers but measured
-// slower on C3: 41.6 vs 35.7 us, with LDS still holding it at 3 workgroups per CU.)
-// One channel's share of a launch: workgroup `bid` of `nb` working on channel p.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
-__device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* __restrict__ tables,
-                                             int64_t bid, int64_t nb) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NT>;
+// One channel's share of a launch: workgroup `bid` of `nb` working on channel p, with the
+// epilogue EM chosen on the host (rx_mfma_em): each kernel keeps only its own stores.
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+__device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* __restrict__ tables, int64_t bid,
+                                             int64_t nb) {
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
     _Float16* pl = lds_h;                                   // 4 sample planes
     _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
@@ -814,76 +857,50 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
         reinterpret_cast<h8*>(tbl)[j] = reinterpret_cast<const h8*>(tables)[j];
     __syncthreads();
     const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;
-#ifndef MODEM_RX_CONTIG
     // Rounds of nb tiles from the top down, tile R - (r + 1) nb + bid in round r. The TX hands
     // its tiles out grid-strided (tile i to workgroup i mod grid, both grids multiples of 8, so
     // tile i is written on XCD slot i mod 8); the RX's first round then reads the ~32 MiB the
     // TX wrote last, each tile on the XCD slot that wrote it (blocks b and b + 8 share an XCD).
-    // C3: 35.0 -> 33.8 us, A/B twice on one box against contiguous ranges per workgroup
-    // (MODEM_RX_CONTIG; that variant now spills 28 B/lane, 37-38 us). The XCD match is what
-    // pays: the same rounds with the slots shifted by 1 or 4 (MODEM_RX_XCD_SHIFT) measured
-    // 38.1-39.1 us. PMC FETCH_SIZE per launch is unchanged (139 vs 137 MB).
+    // C3: 35.0 -> 33.8 us against contiguous ranges per workgroup; the same rounds with the
+    // slots shifted by 1 or 4 measured 38.1-39.1 us (PMC FETCH_SIZE per launch unchanged).
     const int64_t R = (ntiles + nb - 1) / nb * nb;
-#ifdef MODEM_RX_XCD_SHIFT     // experiment: the same rounds with the XCD slots mismatched
-    TileSeq sq{R - nb + (bid + MODEM_RX_XCD_SHIFT) % nb, -nb, R / nb};
-#else
     TileSeq sq{R - nb + bid, -nb, R / nb};
-#endif
     if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }
-#else
-    const int64_t t0 = ntiles * bid / nb, t1 = ntiles * (bid + 1) / nb;
-    const TileSeq sq{t0, 1, t1 - t0};
-#endif
     if (sq.count <= 0) return;
-#ifdef MODEM_STAGGER
-    // workgroups dealt to the same CU (b, b + CUs, ...) start a fraction of a tile apart so
-    // their staging (VALU) and matrix phases interleave instead of running in lockstep
-    {
-        const int k = (int)(bid / MODEM_STAGGER) % 3;
-        for (int i = 0; i < k * 12; ++i) __builtin_amdgcn_s_sleep(127);   // ~8K cycles each step
-    }
-#endif
-    // f32 input with the complex mix (the loopback chain): the epilogue is specialised on what
-    // it stores, so the tile loop's store count is static. Other variants share the guarded one.
-    if (std::is_same<InT, float>::value && MIX == MIX_COMPLEX) {
-        const bool qam = p.slicer_kind == SLICER_QAM_AXIS && p.out_sym;
-        if (p.out_iq && qam) { K::template run<RXE_IQSYM>(p, pl, tbl, red, sq); return; }
-        if (p.out_iq && p.out_sym && p.slicer_kind == SLICER_NEAREST) {
-            K::template run<RXE_IQSYM | RXE_NEAREST>(p, pl, tbl, red, sq);
-            return;
-        }
-        if (p.out_iq && !p.out_sym) { K::template run<RXE_IQ>(p, pl, tbl, red, sq); return; }
-        if (!p.out_iq && qam) { K::template run<RXE_SYM>(p, pl, tbl, red, sq); return; }
-    }
-    // f16 storage of the loopback chain (C5 f16): I/Q and QAM decisions, unconditional stores
-    if (std::is_same<InT, __half>::value && MIX == MIX_COMPLEX && p.out_iq && p.out_sym &&
-        p.slicer_kind == SLICER_QAM_AXIS) {
-        K::template run<RXE_IQSYM>(p, pl, tbl, red, sq);
-        return;
-    }
-    K::template run<RXE_GEN>(p, pl, tbl, red, sq);
+    K::template run<EM>(p, pl, tbl, red, sq, bid);
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NT>::WPE)))
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT>::WPE)))
 void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NT>(p, tables, blockIdx.x, gridDim.x);
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, EM>(p, tables, blockIdx.x, gridDim.x);
 }
 
 // A batch of independent channels of one configuration (modem_rx_process_batch): workgroup
 // b serves channel b / g as its workgroup b % g of g.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NT>::WPE)))
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT>::WPE)))
 void rx_mfma_batch(const RxBatch b, const _Float16* __restrict__ tables) {
-#ifdef MODEM_BATCH_INTERLEAVE
-    const int ch = (int)(blockIdx.x % (unsigned)b.nch);
-    const unsigned bid = blockIdx.x / (unsigned)b.nch;
-#else
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
     const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
-#endif
     const RxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NT>(p, tables, bid, b.g);
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, EM>(p, tables, bid, b.g);
+}
+
+// The epilogue specialisation for a call: stores known at compile time for the loopback
+// chain's outputs (f32 or f16 I/Q in and out, complex mix), else the guarded general one.
+template <typename InT, int MIX, typename OutT>
+__host__ inline int rx_mfma_em(const RxParams& p) {
+    const bool loop = std::is_same<InT, OutT>::value && MIX == MIX_COMPLEX;
+    if (!loop) return RXE_GEN;
+    const bool qam = p.slicer_kind == SLICER_QAM_AXIS && p.out_sym;
+    if (p.out_iq && qam) return RXE_IQSYM;
+    if (std::is_same<InT, float>::value) {
+        if (p.out_iq && p.out_sym && p.slicer_kind == SLICER_NEAREST) return RXE_IQSYM | RXE_NEAREST;
+        if (p.out_iq && !p.out_sym) return RXE_IQ;
+        if (!p.out_iq && qam) return RXE_SYM;
+    }
+    return RXE_GEN;
 }
 
 // Any decimation: thread per kept instant, mixed samples staged in natural order.
@@ -949,44 +966,64 @@ static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s
                                      : rx_dec<InT, MIX_COMPLEX, OutT>(p, decim, s);
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NT>
-static hipError_t rxm_go_nt(const RxParams& p, const void* tables, hipStream_t s) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NT>;
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+static hipError_t rxm_go_em(const RxParams& p, const void* tables, hipStream_t s) {
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
     const int64_t ntiles = (p.nout + (p.k_first & 15) + K::TS - 1) / K::TS;
-    const size_t lds = K::LDS_BYTES;
-    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, NT>);
-    static const int cap = env_wgs_per_cu("MODEM_RX_WGS_PER_CU");
-    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, NT>), dim3(persistent_grid(k, K::NT, lds, ntiles, cap)),
-                       dim3(K::NT), lds, s, p, static_cast<const _Float16*>(tables));
+    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, EM>);
+    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, EM>), dim3(persistent_grid(k, K::NT, K::LDS_BYTES, ntiles)),
+                       dim3(K::NT), K::LDS_BYTES, s, p, static_cast<const _Float16*>(tables));
     return hipGetLastError();
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT>
-static hipError_t rxm_go(const RxParams& p, const void* tables, hipStream_t s) {
-#ifdef MODEM_RX_NT64
-    return rxm_go_nt<DEC, NKS, InT, MIX, OutT, 64>(p, tables, s);
-#else
-    return rxm_go_nt<DEC, NKS, InT, MIX, OutT, 256>(p, tables, s);
-#endif
-}
-
-template <int DEC, int NKS, typename InT, typename OutT>
-static hipError_t rxm_go_batch(RxBatch b, const void* tables, hipStream_t s) {
-    using K = RxMfma<DEC, NKS, InT, MIX_COMPLEX, OutT, 256>;
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+static hipError_t rxm_go_batch_em(RxBatch b, const void* tables, hipStream_t s) {
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
     int64_t ntiles = 0;
     for (int c = 0; c < b.nch; ++c) {
         const int64_t t = (b.p[c].nout + (b.p[c].k_first & 15) + K::TS - 1) / K::TS;
         ntiles = t > ntiles ? t : ntiles;
     }
-    const size_t lds = K::LDS_BYTES;
-    const void* k = reinterpret_cast<const void*>(&rx_mfma_batch<DEC, NKS, InT, MIX_COMPLEX, OutT, 256>);
-    const int64_t cap = persistent_grid(k, K::NT, lds, INT64_MAX);
+    const void* k = reinterpret_cast<const void*>(&rx_mfma_batch<DEC, NKS, InT, MIX, OutT, EM>);
+    const int64_t cap = persistent_grid(k, K::NT, K::LDS_BYTES, INT64_MAX);
     int64_t g = cap / b.nch;
     g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
     b.g = (int32_t)g;
-    hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX_COMPLEX, OutT, 256>), dim3((unsigned)(g * b.nch)),
-                       dim3(K::NT), lds, s, b, static_cast<const _Float16*>(tables));
+    hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX, OutT, EM>), dim3((unsigned)(g * b.nch)),
+                       dim3(K::NT), K::LDS_BYTES, s, b, static_cast<const _Float16*>(tables));
     return hipGetLastError();
+}
+
+// Dispatch on the epilogue: the specialised ones exist only where rx_mfma_em can pick them.
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, bool BATCH, typename Arg>
+static hipError_t rxm_em(const Arg& a, int em, const void* tables, hipStream_t s) {
+    constexpr bool loop = std::is_same<InT, OutT>::value && MIX == MIX_COMPLEX;
+    constexpr bool f32 = std::is_same<InT, float>::value;
+    auto go = [&](auto emc) {
+        constexpr int E = decltype(emc)::value;
+        if constexpr (BATCH) return rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, E>(a, tables, s);
+        else return rxm_go_em<DEC, NKS, InT, MIX, OutT, E>(a, tables, s);
+    };
+    switch (em) {
+    case RXE_IQSYM: return go(std::integral_constant<int, loop ? RXE_IQSYM : RXE_GEN>());
+    case RXE_IQSYM | RXE_NEAREST: return go(std::integral_constant<int, loop && f32 ? (RXE_IQSYM | RXE_NEAREST) : RXE_GEN>());
+    case RXE_IQ: return go(std::integral_constant<int, loop && f32 ? RXE_IQ : RXE_GEN>());
+    case RXE_SYM: return go(std::integral_constant<int, loop && f32 ? RXE_SYM : RXE_GEN>());
+    default: return go(std::integral_constant<int, RXE_GEN>());
+    }
+}
+
+template <int DEC, int NKS, typename InT, int MIX, typename OutT>
+static hipError_t rxm_go(const RxParams& p, const void* tables, hipStream_t s) {
+    return rxm_em<DEC, NKS, InT, MIX, OutT, false>(p, rx_mfma_em<InT, MIX, OutT>(p), tables, s);
+}
+
+template <int DEC, int NKS, typename InT, typename OutT>
+static hipError_t rxm_go_batch(const RxBatch& b, const void* tables, hipStream_t s) {
+    int em = rx_mfma_em<InT, MIX_COMPLEX, OutT>(b.p[0]);          // one epilogue for the batch
+    for (int c = 1; c < b.nch; ++c)
+        if (rx_mfma_em<InT, MIX_COMPLEX, OutT>(b.p[c]) != em) em = RXE_GEN;
+    return rxm_em<DEC, NKS, InT, MIX_COMPLEX, OutT, true>(b, em, tables, s);
 }
 
 // (decim, k-steps) variants: W = 32 * nks >= 15 * decim + ntaps.
@@ -1062,10 +1099,3 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
 
 }  // namespace mk
 
-#ifdef MODEM_STAMPS
-// Diagnostic builds only (tools/stamps.py): the per-wave segment cycle sums of the stamped
-// RX launches (same translation unit as the kernel that writes them).
-extern "C" int modem_debug_stamps(unsigned long long* host, size_t n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(mk::g_stamps), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
-}
-#endif

@@ -287,20 +287,12 @@ template <int SPS> struct TxMfmaCfg {
 };
 
 // Carrier mix of one sample, packed: (re, im) = (y*cs - yi*sn, y*sn + yi*cs), y = (yr, yi),
-// cssn = (cs, sn) straight from v_sin/v_cos (hence the wait state, see cmix in modem_rx.hip).
+// cssn = (cs, sn) straight from v_sin/v_cos.
 __device__ __forceinline__ cf2 tx_cmix(cf2 y, cf2 cssn) {
-#ifdef MODEM_CMIX_ASM
-    cf2 t, z;
-    asm("s_nop 0\n\tv_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(y), "v"(cssn));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]"
-        : "=v"(z) : "v"(y), "v"(cssn), "v"(t));
-    return z;
-#else
     // vector ops (v_pk_mul_f32 + v_pk_fma_f32 with op_sel / neg modifiers): visible to the
     // compiler's hazard recognizer, which pads only where a v_sin/v_cos result is read too early
     const cf2 t = y * cssn.xx;
     return __builtin_elementwise_fma(y.yx, (cf2){-cssn.y, cssn.y}, t);
-#endif
 }
 
 typedef _Float16 th8 __attribute__((ext_vector_type(8)));

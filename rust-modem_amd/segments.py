@@ -87,14 +87,33 @@ def rx_segment(na: int, nb: int, ntaps: int, sps: int, align: int = ALIGN_SYMBOL
     return {"s0": n0, "input": (n0, nb), "drop": k_lo - n0 // sps, "instants": (k_lo, k_hi)}
 
 
+# Phasors that carry state from symbol to symbol in f32 (DMPSK phase, dmpsk.rs:29-33; MFSK
+# cur_coef / phase_offset, mfsk.rs:68-75; BFSK phase / previous bit, bfsk.rs:43-55): a handle
+# started a halo early begins from the initial state, not the state the long stream has at the
+# halo, so a time segment other than the first would come out wrong. They are not sharded.
+SERIAL_STATE_PHASORS = ("DMPSK", "MFSK", "BFSK")
+
+
+def _to_device(x, device):
+    """The slice on `device` (a handle's kernels only read their own device's memory)."""
+    if type(x).__module__.startswith("torch") and x.is_cuda and x.device.index != device:
+        return x.to(f"cuda:{device}")
+    return x
+
+
 def run_tx_segment(pkg, carrier_freq, phasor, taps, sps, bits, a, b, dtype=0, device=0, stream=None):
     """TX samples [a * sps, b * sps) of the stream whose bits are `bits` (one byte per bit,
-    the whole stream's buffer), through a fresh DigitalModulator started a halo early."""
+    the whole stream's buffer), through a fresh DigitalModulator started a halo early.
+    Raises ValueError for phasors with serial symbol state (SERIAL_STATE_PHASORS) unless the
+    segment starts at symbol 0."""
+    if type(phasor).__name__ in SERIAL_STATE_PHASORS and a > 0:
+        raise ValueError(f"{type(phasor).__name__} carries its phase from symbol to symbol: "
+                         "a time segment cannot start mid-stream")
     plan = tx_segment(a, b, len(taps), sps, phasor.bits_per_symbol())
     mod = pkg.DigitalModulator(pkg.Carrier(carrier_freq, plan["s0"]), phasor, sps, taps=taps, dtype=dtype,
                                device=device)
     lo, hi = plan["bits"]
-    y = mod.process(bits[lo:hi], stream=stream)
+    y = mod.process(_to_device(bits[lo:hi], device), stream=stream)
     return y[plan["drop"]:]
 
 
@@ -106,6 +125,6 @@ def run_rx_segment(pkg, carrier_freq, taps, sps, slicer, x, na, nb, in_dtype=0, 
     rx = pkg.DemodulatorRx(pkg.Carrier(carrier_freq, plan["s0"]), taps, decim=sps, decim_offset=len(taps) - 1,
                            mix=pkg.MIX_COMPLEX, slicer=slicer, in_dtype=in_dtype, out_dtype=in_dtype, device=device)
     lo, hi = plan["input"]
-    iq, sym = rx.process(x[lo:hi], stream=stream)
+    iq, sym = rx.process(_to_device(x[lo:hi], device), stream=stream)
     d = plan["drop"]
     return iq[d:], sym[d:], plan["instants"]

@@ -224,3 +224,42 @@ def test_batch_entry_argument_checks(m):
     prod = (sz * 1)()
     assert L.modem_tx_process_batch(None, 1, None, None, None, None, prod, None) == -1
     assert L.modem_rx_process_batch(None, 1, None, None, None, None, None, prod, None) == -1
+
+
+def _layout_binary(tmp_path):
+    """tests/cpp/abi_layout (built by build(); compiled here if absent). Its static_asserts
+    are the table; compiling it is half the test."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "cpp", "abi_layout")
+    if not os.path.exists(exe):
+        exe = str(tmp_path / "abi_layout")
+        subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "cpp", "abi_layout.c"), "-o", exe], check=True)
+    return subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+
+
+def test_descriptor_layouts_match_integration_table(tmp_path):
+    """Every descriptor's size, alignment and field offsets (as the C compiler lays them out)
+    equal the table in INTEGRATION.md that the Rust #[repr(C)] structs follow."""
+    got = {}
+    for line in _layout_binary(tmp_path).split("\n"):
+        if line:
+            k, *v = line.split()
+            got[k] = tuple(int(x) for x in v)
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    rows = re.findall(r"^\| `(modem_[a-z_]+)` \| (\d+) \| (\d+) \| ([^|]+) \|$", text, flags=re.M)
+    assert {r[0] for r in rows} == {"modem_ring", "modem_phasor_desc", "modem_slicer_desc",
+                                    "modem_tx_desc", "modem_rx_desc"}
+    for name, size, align, fields in rows:
+        assert got[name] == (int(size), int(align)), name
+        doc = [f.strip().rsplit(" ", 1) for f in fields.split(",")]
+        built = [(k.split(".", 1)[1], v[0]) for k, v in got.items() if k.startswith(name + ".")]
+        assert [(f, int(o)) for f, o in doc] == built, name
+
+
+def test_header_compiles_as_cpp(tmp_path):
+    """The same layout asserts through g++ (the header's extern "C" path)."""
+    import subprocess
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-x", "c++",
+                    "-c", os.path.join(ROOT, "tests", "cpp", "abi_layout.c"), "-o", str(tmp_path / "a.o")],
+                   check=True)

@@ -50,8 +50,8 @@ class CpuRunner:
     def sync(self):
         pass
 
-    def kernel_times_ms(self, reps):
-        return 0.01, 0.02
+    def kernel_times_ms(self, reps, rounds=5):
+        return 0.01, 0.02, 0.03
 
     def check(self):
         sent = self.bits[0].reshape(-1, self.bps).astype(np.int64) @ (1 << np.arange(self.bps)[::-1])
@@ -67,7 +67,8 @@ def _worker(rank, world, port, outdir):
     import oracle as o
     td.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     bench.WORKLOADS["tiny"] = ("qam16", 4, 129, 4, 1 << 12, 2, 0, "tiny: 2 channels x 4096 samples")
-    args = bench.argparse.Namespace(config="tiny", steps=3, warmup=1, no_cpu_baseline=True, cpu_samples=0)
+    args = bench.argparse.Namespace(config="tiny", steps=3, warmup=1, no_cpu_baseline=True, cpu_samples=0,
+                                    amplitude=1.0, no_out_of_cache=True)
     runners = []
 
     def factory(wl, r):

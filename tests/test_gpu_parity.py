@@ -414,3 +414,18 @@ def test_batch_plans_equal_single_calls(m, o, torch_cuda):
             giq, gsym = single[c][1].process(y)
             assert got[c] == giq.shape[0]
             assert torch.equal(iqs[c][: got[c]], giq) and torch.equal(syms[c][: got[c]], gsym), (period, c)
+
+
+# ------------------------------------------------------------------ C host ----
+def test_c_host_loopback():
+    """tests/cpp/loopback.c: the C ABI from a plain C program (host buffers, split calls,
+    flushes), every decision equal to the symbol sent."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    exe = os.path.join(ROOT, "tests", "cpp", "loopback")
+    assert os.path.exists(exe), "tests/cpp/loopback not built (build())"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=90)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0
+    assert "0 wrong" in r.stdout

@@ -2,10 +2,10 @@
 # Build ablation variants of the backend (profiling only) into rust-modem_amd/build/ablate/<v>/.
 # Each variant drops one stage of the kernels so its cost shows up as a time difference:
 # FIR (no matrix products), TRIG (no sin/cos), MIX (no carrier mix at all), STORE (no
-# output stores), LOAD (RX: no input loads). Usage: tools/ablate.sh [variants...]
+# output stores; TX only). Usage: tools/ablate.sh [variants...]
 set -e
 cd "$(dirname "$0")/../rust-modem_amd"
-vars=${@:-base FIR TRIG MIX STORE LOAD}
+vars=${@:-base FIR TRIG MIX STORE}
 for v in $vars; do
   d=build/ablate/$v; mkdir -p $d
   extra=""; [ "$v" != base ] && extra="-DMODEM_ABLATE_$v"

@@ -16,8 +16,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", choices=["tx", "rx", "both"], default="both")
+    ap.add_argument("--amplitude", type=float, default=1.0)
     a = ap.parse_args()
-    r = bench.GpuRunner(bench.WORKLOADS[a.config], 0, 0)
+    r = bench.GpuRunner(bench.WORKLOADS[a.config], 0, 0, amplitude=a.amplitude)
     for _ in range(a.reps):
         for c in range(r.nch):
             if a.only in ("tx", "both"):
