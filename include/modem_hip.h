@@ -50,7 +50,8 @@ extern "C" {
 #endif
 
 /* 2: modem_tx_desc.q_offset; 3: the channel-batch entry points; 4: modem_rx_desc.phase_offset
- * (the descriptor grew 8 bytes: 80 -> 88) and modem_pll_lock. Layouts: INTEGRATION.md. */
+ * (the descriptor grew 8 bytes: 80 -> 88), modem_pll_lock, MODEM_DTYPE_I16 and
+ * MODEM_MIX_REFERENCE_REAL_EXACT. Layouts: INTEGRATION.md. */
 #define MODEM_HIP_ABI_VERSION 4
 
 typedef enum {
@@ -63,7 +64,9 @@ typedef enum {
     MODEM_ERR_ALLOC = -6          /* host or device allocation failed */
 } modem_status;
 
-typedef enum { MODEM_DTYPE_F32 = 0, MODEM_DTYPE_F16 = 1 } modem_dtype;
+/* I16: real-valued samples, one native-endian int16 per sample (what `demodulate` reads from
+ * stdin, bin/util.rs:3-37); RX input only, with MODEM_MIX_REFERENCE_REAL_EXACT. */
+typedef enum { MODEM_DTYPE_F32 = 0, MODEM_DTYPE_F16 = 1, MODEM_DTYPE_I16 = 2 } modem_dtype;
 
 /* TX output: complex (i,q)*e^{j phase} (IQSample::modulate, modulator.rs:45-48); the
  * un-mixed baseband (what `modulate --iq` writes, modulate.rs:110-113); or only the real
@@ -75,8 +78,12 @@ typedef enum {
 } modem_out_mode;
 
 /* RX mix: complex conjugate x*e^{-j phase} (loopback contract), or the reference's
- * real-input mix x.re*(cos, -sin) with the 2x gain (demodulator.rs:46,52-55). */
-typedef enum { MODEM_MIX_COMPLEX = 0, MODEM_MIX_REFERENCE_REAL = 1 } modem_mix;
+ * real-input mix x.re*(cos, -sin) with the 2x gain (demodulator.rs:46,52-55). REAL_EXACT is
+ * the latter with every f32 operation of the reference in its order: glibc's cosf / sinf
+ * results (the libm Rust's f32::cos / sin call on x86-64 Linux), the products, and
+ * FIRFilter::add's sequential fold (fir.rs:18-34) — outputs bit-identical to Demodulator's
+ * (demodulator.rs:44-56). A VALU kernel: for the text front-end, not for throughput. */
+typedef enum { MODEM_MIX_COMPLEX = 0, MODEM_MIX_REFERENCE_REAL = 1, MODEM_MIX_REFERENCE_REAL_EXACT = 2 } modem_mix;
 
 typedef enum {
     MODEM_SLICER_NONE = 0,        /* no decisions */
@@ -258,7 +265,8 @@ modem_status modem_pll_lock(float sample_freq, uint64_t s0, const float* x_iq, s
 /* ---- FIRFilter: real-valued causal FIR over a stream (fir.rs:3-35) ---------------------- */
 typedef struct modem_fir modem_fir;
 modem_status modem_fir_create(const float* taps, uint32_t ntaps, int device, modem_fir** out);
-/* out[i] = FIRFilter::add(in[i]) for consecutive samples (f32, same count in and out). */
+/* out[i] = FIRFilter::add(in[i]) for consecutive samples (f32, same count in and out),
+ * bit-identical: the reference's fold order, separate multiply and add. */
 modem_status modem_fir_process(modem_fir* h, const float* in, float* out, size_t n, void* stream);
 modem_status modem_fir_destroy(modem_fir* h);
 

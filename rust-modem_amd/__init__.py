@@ -34,17 +34,17 @@ __all__ = [
     "Freq", "Rates", "Carrier", "Ring",
     "BPSK", "QPSK", "QAM", "BASK", "MPSK", "APSK", "OQPSK",
     "rrc_taps", "DigitalModulator", "DemodulatorRx", "FIRFilter", "prng_bits",
-    "MIX_COMPLEX", "MIX_REFERENCE_REAL", "OUT_IQ_MIXED", "OUT_IQ_BASEBAND", "OUT_REAL",
-    "TxBatchPlan", "RxBatchPlan", "SLICER_NONE", "SLICER_NEAREST", "SLICER_QAM_AXIS", "DTYPE_F32", "DTYPE_F16",
+    "MIX_COMPLEX", "MIX_REFERENCE_REAL", "MIX_REFERENCE_REAL_EXACT", "OUT_IQ_MIXED", "OUT_IQ_BASEBAND", "OUT_REAL",
+    "TxBatchPlan", "RxBatchPlan", "SLICER_NONE", "SLICER_NEAREST", "SLICER_QAM_AXIS", "DTYPE_F32", "DTYPE_F16", "DTYPE_I16",
 ]
 
 PI32 = float(np.float32(math.pi))      # std::f32::consts::PI
 
 MODEM_OK, ERR_INVALID_ARG, ERR_UNSUPPORTED, ERR_HIP, ERR_NO_DEVICE, ERR_CAPACITY, ERR_ALLOC = (
     0, -1, -2, -3, -4, -5, -6)
-DTYPE_F32, DTYPE_F16 = 0, 1
+DTYPE_F32, DTYPE_F16, DTYPE_I16 = 0, 1, 2   # I16: real samples, RX input (demodulate)
 OUT_IQ_MIXED, OUT_IQ_BASEBAND, OUT_REAL = 0, 1, 2
-MIX_COMPLEX, MIX_REFERENCE_REAL = 0, 1
+MIX_COMPLEX, MIX_REFERENCE_REAL, MIX_REFERENCE_REAL_EXACT = 0, 1, 2
 SLICER_NONE, SLICER_NEAREST, SLICER_QAM_AXIS = 0, 1, 2
 _PH_BPSK, _PH_QPSK, _PH_QAM, _PH_BASK, _PH_MPSK, _PH_APSK, _PH_OQPSK = 1, 2, 3, 4, 5, 6, 7
 
@@ -779,11 +779,14 @@ class Demodulator:
     (demodulate.rs:29-43): `lock_phase(sig)` runs PLL::handle (pll.rs:16-22) over the first 64
     complex samples (host, modem_pll_lock: 64 serial steps of control logic), then `process`
     gives (2*FIR(x.re*cos), 2*FIR(-x.re*sin)) at every further sample on the GPU with the locked
-    offset (`phase = carrier.next() + pll.phase_offset`, demodulator.rs:50).
-    `sig`: (n, 2) float32 (re, im) — a CUDA tensor or a numpy array."""
+    offset (`phase = carrier.next() + pll.phase_offset`, demodulator.rs:50) — by default with
+    MIX_REFERENCE_REAL_EXACT, bit-identical to the reference (exact=False: the fast real mix,
+    within 1e-5). `sig`: (n, 2) float32 (re, im) — a CUDA tensor or a numpy array — or, for
+    `process`, (n,) int16 real samples."""
 
-    def __init__(self, carrier: Carrier, lowpass: np.ndarray, device: int = 0):
+    def __init__(self, carrier: Carrier, lowpass: np.ndarray, device: int = 0, exact: bool = True):
         self.carrier, self.lowpass, self.device = carrier, np.ascontiguousarray(lowpass, np.float32), device
+        self.exact = exact
         self.phase_offset = 0.0
         self._rx = None
 
@@ -803,8 +806,10 @@ class Demodulator:
     def process(self, sig, stream=None):
         """(n, 2) float32 (i, q), one per input sample (Iterator::next, demodulator.rs:44-56)."""
         if self._rx is None:
+            i16 = str(getattr(sig, "dtype", "")).endswith("int16")
             self._rx = DemodulatorRx(self.carrier, self.lowpass, decim=1, decim_offset=0,
-                                     mix=MIX_REFERENCE_REAL, device=self.device,
+                                     mix=MIX_REFERENCE_REAL_EXACT if self.exact else MIX_REFERENCE_REAL,
+                                     in_dtype=DTYPE_I16 if i16 else DTYPE_F32, device=self.device,
                                      phase_offset=self.phase_offset)
         iq, _ = self._rx.process(sig, want_sym=False, stream=stream)
         return iq

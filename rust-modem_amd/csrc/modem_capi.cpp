@@ -745,7 +745,9 @@ struct modem_rx {
     }
 };
 
-static size_t rx_in_bytes(const modem_rx* h) { return h->in_dtype == MODEM_DTYPE_F16 ? 4 : 8; }
+static size_t rx_in_bytes(const modem_rx* h) {
+    return h->in_dtype == MODEM_DTYPE_I16 ? 2 : h->in_dtype == MODEM_DTYPE_F16 ? 4 : 8;
+}
 static size_t rx_out_bytes(const modem_rx* h) { return h->out_dtype == MODEM_DTYPE_F16 ? 4 : 8; }
 
 modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out) {
@@ -753,9 +755,12 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
     *out = nullptr;
     if (d->ntaps < 1 || d->ntaps > (uint32_t)mk::kMaxTaps || !d->taps) return MODEM_ERR_INVALID_ARG;
     if (d->decim < 1) return MODEM_ERR_INVALID_ARG;
-    if (d->mix != MODEM_MIX_COMPLEX && d->mix != MODEM_MIX_REFERENCE_REAL) return MODEM_ERR_INVALID_ARG;
-    if ((d->in_dtype != MODEM_DTYPE_F32 && d->in_dtype != MODEM_DTYPE_F16) ||
+    if (d->mix != MODEM_MIX_COMPLEX && d->mix != MODEM_MIX_REFERENCE_REAL && d->mix != MODEM_MIX_REFERENCE_REAL_EXACT)
+        return MODEM_ERR_INVALID_ARG;
+    if ((d->in_dtype != MODEM_DTYPE_F32 && d->in_dtype != MODEM_DTYPE_F16 && d->in_dtype != MODEM_DTYPE_I16) ||
         (d->out_dtype != MODEM_DTYPE_F32 && d->out_dtype != MODEM_DTYPE_F16)) return MODEM_ERR_INVALID_ARG;
+    // real i16 input: the exact reference demodulator only (the complex kernels read I/Q pairs)
+    if (d->in_dtype == MODEM_DTYPE_I16 && d->mix != MODEM_MIX_REFERENCE_REAL_EXACT) return MODEM_ERR_UNSUPPORTED;
     const modem_slicer_desc& sl = d->slicer;
     if (sl.kind == MODEM_SLICER_NEAREST && (sl.bits_per_symbol < 1 || sl.bits_per_symbol > 8 || !sl.lut))
         return MODEM_ERR_INVALID_ARG;
@@ -808,7 +813,8 @@ modem_status modem_rx_create(const modem_rx_desc* d, int device, modem_rx** out)
     }
     const char* env = std::getenv("MODEM_HIP_FIR");
     const bool force_valu = env && std::strcmp(env, "valu") == 0;
-    h->mfma_ksteps = force_valu ? 0 : mk::rx_mfma_ksteps((int)h->decim, (int)h->ntaps);
+    const bool exact = h->mix == MODEM_MIX_REFERENCE_REAL_EXACT;
+    h->mfma_ksteps = force_valu || exact ? 0 : mk::rx_mfma_ksteps((int)h->decim, (int)h->ntaps);
     if (h->mfma_ksteps > 0) {
         // Split-f16 tap tables of rx_mfma (modem_rx.hip): the reversed taps T[x] = h[W-1-x]
         // scaled by 2^kb (exact; 0 when max |h| is in [2^-3, 2^15), else into [2^14, 2^15)), as f16

@@ -5,10 +5,13 @@
 namespace mk {
 
 // ------------------------------------------------------------------- FIRFilter (real) ----
-// y[n] = sum_{k<L} h[k] x[n-k] (fir.rs:18-34); 256 lanes x 16 outputs per workgroup.
+// y[n] = ((0 + h[0] x[n]) + h[1] x[n-1]) + ... (fir.rs:18-34: FIRFilter::calc folds from the
+// newest sample, one f32 multiply and one f32 add per tap, no fusion) — bit-identical to
+// FIRFilter::add. 256 lanes x 16 outputs per workgroup.
 constexpr int kFirR = 16, kFirNT = 256, kFirTS = kFirR * kFirNT;
 
 __global__ __launch_bounds__(256) void fir_real(const FirParams p) {
+#pragma clang fp contract(off)
     extern __shared__ __attribute__((aligned(16))) float flds[];
     const int tid = threadIdx.x, L = p.L;
     if (blockIdx.x == 0)
@@ -37,7 +40,7 @@ __global__ __launch_bounds__(256) void fir_real(const FirParams p) {
         for (int c = 0; c < 8; ++c) {
             const float h = taps[k + c];
 #pragma unroll
-            for (int r = 0; r < kFirR; ++r) acc[r] = __builtin_fmaf(win[r], h, acc[r]);
+            for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + win[r] * h;
 #pragma unroll
             for (int r = kFirR - 1; r > 0; --r) win[r] = win[r - 1];
             win[0] = base[-(k + c + 1)];
@@ -46,7 +49,7 @@ __global__ __launch_bounds__(256) void fir_real(const FirParams p) {
     for (; k < L; ++k) {
         const float h = taps[k];
 #pragma unroll
-        for (int r = 0; r < kFirR; ++r) acc[r] = __builtin_fmaf(win[r], h, acc[r]);
+        for (int r = 0; r < kFirR; ++r) acc[r] = acc[r] + win[r] * h;
 #pragma unroll
         for (int r = kFirR - 1; r > 0; --r) win[r] = win[r - 1];
         win[0] = base[-(k + 1)];

@@ -9,6 +9,7 @@
 //        with one sliding window per plane (ds_read_b64 per R complex MACs);
 //     3. hard decision + store.
 #include "modem_device.h"
+#include "libm_sincosf.h"
 
 namespace mk {
 
@@ -57,7 +58,17 @@ template <> struct InIO<__half> {
     }
 };
 
-enum { MIX_COMPLEX = 0, MIX_REFERENCE_REAL = 1 };
+// Real int16 samples (MODEM_DTYPE_I16, the `demodulate` reader): x = (v, 0).
+template <> struct InIO<int16_t> {
+    __device__ static float2 load(const void* x, int64_t q) {
+        return make_float2((float)reinterpret_cast<const int16_t*>(x)[q], 0.f);
+    }
+    __device__ static void copy(void* dst, int64_t i, const void* src, int64_t q) {
+        reinterpret_cast<int16_t*>(dst)[i] = reinterpret_cast<const int16_t*>(src)[q];
+    }
+};
+
+enum { MIX_COMPLEX = 0, MIX_REFERENCE_REAL = 1, MIX_REFERENCE_REAL_EXACT = 2 };
 enum { SLICER_NONE = 0, SLICER_NEAREST = 1, SLICER_QAM_AXIS = 2 };
 
 // Sample q of the chunk (q < 0: history; q >= N: past the chunk, zero).
@@ -449,6 +460,12 @@ __device__ __forceinline__ uint8_t rx_slice_qam2(const RxParams& p, float re, fl
 // wave votes with three ballots whether the tile's max lies in that exponent's window. A tile
 // outside it, and the call's first tile (its window reads the history), take the general
 // path: per-sample loads, two passes, the same tile_ka -> identical results either way.
+#ifndef RXLD_AUX
+#define RXLD_AUX 0
+#endif
+#ifndef RXST_AUX
+#define RXST_AUX 0
+#endif
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
 struct RxMfma {
     using Q = Quad<InT>;
@@ -546,11 +563,11 @@ struct RxMfma {
         constexpr int S = sizeof(InT) * 2;
         const int o = voff + 4 * NT * u * S;
         if constexpr (std::is_same<InT, float>::value) {
-            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
-            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, 0));
+            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, RXLD_AUX));
+            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, RXLD_AUX));
             return QT{make_float4(a[0], a[1], a[2], a[3]), make_float4(b[0], b[1], b[2], b[3])};
         } else {
-            return __builtin_bit_cast(QT, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+            return __builtin_bit_cast(QT, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, RXLD_AUX));
         }
     }
 
@@ -695,14 +712,14 @@ struct RxMfma {
             const float a = re[r] * GAIN, b = im[r] * GAIN;
             if (EM & RXE_IQ) {
                 if constexpr (std::is_same<OutT, float>::value)
-                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(a, b)), riq, 8 * off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(a, b)), riq, 8 * off, 0, RXST_AUX);
                 else
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, __floats2half2_rn(a, b)), riq, 4 * off, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, __floats2half2_rn(a, b)), riq, 4 * off, 0, RXST_AUX);
             }
             if (EM & RXE_SYM) {
                 const uint8_t sy = !(EM & RXE_NEAREST) ? rx_slice_qam2(p, a, b)
                                  : p.bps == 2 ? rx_slice_nearest4(p, a, b) : rx_slice_nearest(p, a, b);
-                __builtin_amdgcn_raw_buffer_store_b8(sy, rsy, off, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8(sy, rsy, off, 0, RXST_AUX);
             }
         }
     }
@@ -930,6 +947,57 @@ __global__ __launch_bounds__(64) void rx_generic(const RxParams p) {
     rx_emit<OutT>(p, o, g * yr, g * yi);
 }
 
+// Bit-exact reference demodulator (MODEM_MIX_REFERENCE_REAL_EXACT; demodulator.rs:44-56 at the
+// kept instants): every f32 operation of the reference in its order. Per staged sample
+// phase = Carrier::next() + pll.phase_offset (one f32 add), (c, s) = glibc's cosf / sinf
+// (lm::, the library Rust's f32::cos / sin call), z = (x.re * c, x.re * -s); per output the
+// FIRFilter::calc fold (fir.rs:18-34) s = ((0 + z[n] h0) + z[n-1] h1) + ..., separate multiply
+// and add, over a history that is zero before the stream; y = 2 s. Thread per kept instant,
+// ts instants per workgroup, their (ts - 1) * decim + L mixed samples in LDS.
+template <typename InT, typename OutT>
+__global__ __launch_bounds__(256) void rx_exact(const RxParams p, int ts) {
+#pragma clang fp contract(off)
+    extern __shared__ __attribute__((aligned(16))) float2 zl[];
+    const int L = p.L, DEC = p.decim;
+    if (blockIdx.x == 0) rx_state_update<InT>(p);
+    const int64_t o0 = (int64_t)blockIdx.x * ts;
+    if (o0 >= p.nout) return;
+    const int64_t n_lo = (p.k_first + o0) * DEC + p.D - (L - 1);      // stream index of zl[0]
+    const int NS = (ts - 1) * DEC + L;
+    for (int e = threadIdx.x; e < NS; e += blockDim.x) {
+        const int64_t n = n_lo + e;
+        float2 z = make_float2(0.f, 0.f);                              // history before the stream
+        if (n >= 0) {
+            const float x = rx_sample<InT>(p, n - p.n_start).x;       // Complex::re
+            const float ph = rx_phase(p, carrier_phase(p.w, p.c0 + (uint64_t)n, p.exact_idx));
+            z = make_float2(x * lm::cosf<true>(ph), x * -lm::sinf<true>(ph));
+        }
+        zl[e] = z;
+    }
+    __syncthreads();
+    const int j = threadIdx.x;
+    if (j >= ts || o0 + j >= p.nout) return;
+    const float2* zc = zl + j * DEC + (L - 1);                         // the instant's newest sample
+    float si = 0.f, sq = 0.f;
+    for (int t = 0; t < L; ++t) {
+        const float h = p.taps[(t % DEC) * p.K + t / DEC];            // h[t] (polyphase layout)
+        si = si + zc[-t].x * h;
+        sq = sq + zc[-t].y * h;
+    }
+    rx_emit<OutT>(p, o0 + j, 2.0f * si, 2.0f * sq);
+}
+
+template <typename InT, typename OutT>
+static hipError_t rx_exact_go(const RxParams& p, hipStream_t s) {
+    int ts = 256;
+    while (ts > 1 && (size_t)((ts - 1) * p.decim + p.L) * sizeof(float2) > 65536) ts /= 2;
+    const size_t lds = (size_t)((ts - 1) * p.decim + p.L) * sizeof(float2);
+    if (lds > 65536) return hipErrorInvalidValue;
+    const int64_t nblk = (p.nout + ts - 1) / ts;
+    hipLaunchKernelGGL((rx_exact<InT, OutT>), dim3((unsigned)(nblk > 0 ? nblk : 1)), dim3(256), lds, s, p, ts);
+    return hipGetLastError();
+}
+
 
 template <int DEC, typename InT, int MIX, typename OutT>
 static hipError_t rx_go(const RxParams& p, hipStream_t s) {
@@ -1089,6 +1157,14 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
 #ifdef MODEM_DEV_MIN
     return hipErrorInvalidValue;
 #endif
+    if (mix == MIX_REFERENCE_REAL_EXACT) {
+        auto go = [&](auto in_t) {
+            using InT = decltype(in_t);
+            return out_dtype == 1 ? rx_exact_go<InT, __half>(p, s) : rx_exact_go<InT, float>(p, s);
+        };
+        return in_dtype == 2 ? go(int16_t()) : in_dtype == 1 ? go(__half()) : go(float());
+    }
+    if (in_dtype == 2) return hipErrorInvalidValue;
     if (in_dtype == 1)
         return out_dtype == 1 ? rx_mixsel<__half, __half>(p, decim, mix, s)
                               : rx_mixsel<__half, float>(p, decim, mix, s);

@@ -1,37 +1,78 @@
-"""The `demodulate` front-end: demodulate.rs:29-43 — analytic signal
-(x, Hilbert(x)), Demodulator with the 64-sample PLL lock (demodulator.rs:32-36, pll.rs:16-22)
-and the full-rate real-input mix + low-pass (demodulator.rs:44-56) — on the GPU (Hilbert on
-modem_fir, the demodulator on modem_rx with the locked phase offset) against the oracle's
-restatement with the same filters.
+"""The `demodulate` drop-in: demodulate.rs:15-44 — i16 samples on stdin
+(bin/util.rs:3-37), analytic signal (x, Hilbert(x)), Demodulator with the 64-sample PLL lock
+(demodulator.rs:32-36, pll.rs:16-22) and the full-rate real-input mix + low-pass
+(demodulator.rs:44-56), one `i:{}\\tq:{}` line per later sample — against the oracle's
+restatement (or_demodulate_front) with the binary's own filter tables (demodulate.rs:47-150,
+rust-modem_amd/cli/demod_taps.h).
 
-The binary's own coefficient tables (demodulate.rs:47-150) are not copied here: the filters
-are designed in this file (a 23-tap windowed Hilbert and a 64-tap windowed-sinc low-pass with
-the binary's 1 kHz pass band at 10 kHz), so parity covers the structure, not those numbers.
-Tolerance: the PLL offset (host, glibc) bit-exact; outputs within 1e-5 of their maximum.
+Bit-exact throughout: the GPU demodulator runs MODEM_MIX_REFERENCE_REAL_EXACT (glibc's cosf /
+sinf restated in libm_sincosf.h, checked here against the host libm; FIRFilter's fold), the
+Hilbert filter is modem_fir (the same fold), the PLL is host f32 code. The CLI's text is
+compared byte for byte with the oracle's values formatted as Rust's f32 Display (numpy's
+shortest round-trip positional form, an implementation independent of the CLI's to_chars).
 """
 import ctypes
+import os
+import re
+import subprocess
 
 import numpy as np
 import pytest
 
+from conftest import ROOT
 
-def hilbert_taps(n=23):
-    k = np.arange(n) - (n - 1) // 2
-    h = np.where(k % 2 != 0, 2.0 / (np.pi * np.where(k == 0, 1, k)), 0.0)
-    return (h * np.hamming(n)).astype(np.float32)
+TAPS_H = os.path.join(ROOT, "rust-modem_amd", "cli", "demod_taps.h")
+CLI = os.path.join(ROOT, "rust-modem_amd", "bin", "demodulate")
+SR, CF = 10000, 900
 
 
-def lowpass_taps(n=64, fc=1250.0, sr=10000.0):
-    t = np.arange(n) - (n - 1) / 2.0
-    h = 2 * fc / sr * np.sinc(2 * fc / sr * t) * np.hamming(n)
-    return (h / h.sum()).astype(np.float32)
+def reference_tables():
+    """The two tables of demodulate.rs:47-150 as the CLI compiles them (f32 literals)."""
+    text = open(TAPS_H).read()
+
+    def table(name):
+        body = re.search(name + r"\[\d+\] = \{(.*?)\};", text, re.S).group(1)
+        return np.array([float(t.rstrip("f")) for t in body.replace("\n", " ").split(",") if t.strip()],
+                        dtype=np.float32)
+    return table("kDemodHilbert"), table("kDemodLowpass")
+
+
+def rust_display(v: np.float32) -> str:
+    """Rust's `{}` for f32: shortest round-trip digits, positional, no trailing '.0'."""
+    if np.isnan(v):
+        return "NaN"
+    if np.isinf(v):
+        return "inf" if v > 0 else "-inf"
+    return np.format_float_positional(np.float32(v), unique=True, trim="-")
+
+
+def expected_text(o, x16):
+    hil, lp = reference_tables()
+    i, q, _ = o.demodulate_front(o.sample_freq(CF, SR), x16.astype(np.float32), hil, lp)
+    return "".join(f"i:{rust_display(a)}\tq:{rust_display(b)}\n" for a, b in zip(i, q)).encode()
+
+
+def passband_i16(o, nbits=300, seed=77, scale=12000.0):
+    """A BPSK passband (the modulator's real output, modulate.rs:128-133) as i16 samples."""
+    w = o.sample_freq(CF, SR)
+    bits = o.prng_bits(seed, nbits)
+    y = o.tx_chain(o.new_phasor(o.BPSK, np.float32(np.pi / 4), 1.0), bits, 45, None, w, 0,
+                   out_mode=o.OUT_REAL)
+    return np.round(y * scale).astype(np.int16)
+
+
+def test_reference_tables():
+    hil, lp = reference_tables()
+    assert hil.shape == (23,) and lp.shape == (64,)
+    assert hil[11] == 0.0 and hil[12] == np.float32(0.62794) and lp[0] == np.float32(8.6464950643449706e-05)
+    assert np.array_equal(lp, lp[::-1])                      # the low-pass is symmetric
 
 
 def test_pll_lock_matches_oracle(m, o):
     """modem_pll_lock (host) == the oracle's PLL over the same 64 analytic samples."""
     rng = np.random.default_rng(5)
     x = rng.standard_normal((64, 2)).astype(np.float32)
-    w = o.sample_freq(900, 10000)
+    w = o.sample_freq(CF, SR)
     off = (ctypes.c_float * 1)(0.0)
     assert m.load_library().modem_pll_lock(w, 0, m._fptr(np.ascontiguousarray(x)), 64, off) == 0
     p = (ctypes.c_float * 1)(0.0)
@@ -40,35 +81,157 @@ def test_pll_lock_matches_oracle(m, o):
     assert np.float32(off[0]).view(np.uint32) == np.float32(p[0]).view(np.uint32)
 
 
+def _build(tmp_path, name, src_text, extra=()):
+    src = tmp_path / (name + ".cpp")
+    src.write_text(src_text)
+    exe = tmp_path / name
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-Wno-unknown-pragmas",
+                    "-I", os.path.join(ROOT, "rust-modem_amd", "cli"), "-I", os.path.join(ROOT, "rust-modem_amd", "csrc"),
+                    *extra, str(src), "-o", str(exe)], check=True)
+    return str(exe)
+
+
+def test_fmt_f32_is_rust_display(tmp_path):
+    """cli/fmt_f32.h (std::to_chars) prints every value as Rust's Display would (numpy's
+    independent shortest round-trip formatter), specials and 2^18 random bit patterns."""
+    exe = _build(tmp_path, "fmt", r'''
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include "fmt_f32.h"
+int main() {
+    std::vector<float> v;
+    float f;
+    while (std::fread(&f, 4, 1, stdin) == 1) v.push_back(f);
+    char b[80];
+    for (float x : v) { int n = fmt_f32(b, x); b[n] = '\n'; std::fwrite(b, 1, n + 1, stdout); }
+}''')
+    rng = np.random.default_rng(3)
+    special = np.array([0.0, -0.0, 1.0, -1.0, 0.1, 1e-45, -1e-45, 3.4028235e38, 1e20, 123456789.0, 0.5,
+                        2.0 ** -126, 1.17549435e-38, 16777216.0, 16777217.0, np.inf, -np.inf, np.nan],
+                       dtype=np.float32)
+    rnd = rng.integers(0, 2 ** 32, 1 << 18, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    normal = (rng.standard_normal(1 << 16) * 3000).astype(np.float32)
+    vals = np.concatenate([special, rnd, normal])
+    out = subprocess.run([exe], input=vals.tobytes(), capture_output=True, check=True).stdout.decode()
+    got = out.split("\n")[:-1]
+    want = [rust_display(v) for v in vals]
+    bad = [(w, g) for w, g in zip(want, got) if w != g]
+    assert len(got) == len(vals) and not bad, bad[:5]
+
+
+def test_libm_restatement_matches_host_libm(tmp_path):
+    """libm_sincosf.h (the device's sin / cos) against the host's sinf / cosf, bitwise, over
+    every 4099th f32 plus all of [-8, 8] at a stride of 7 ulps (tools/libm_check.cpp checks
+    all 2^32 inputs: 0 mismatches for the FMA build, DESIGN.md)."""
+    exe = _build(tmp_path, "libm_check", open(os.path.join(ROOT, "tools", "libm_check.cpp")).read()
+                 .replace('#include "../rust-modem_amd/csrc/libm_sincosf.h"', '#include "libm_sincosf.h"'),
+                 extra=("-pthread",))
+    r = subprocess.run([exe, "4", "4099"], capture_output=True, text=True)
+    print(r.stdout)
+    assert "sinf fma    mismatches 0" in r.stdout and "cosf fma    mismatches 0" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbits,scale,tail", [(300, 12000.0, b""), (40, 30000.0, b"\x01"), (2, 1.0, b"")])
+def test_demodulate_cli_byte_exact(o, tmp_path, nbits, scale, tail):
+    """bin/demodulate's stdout equals the oracle's lines byte for byte (an odd trailing byte
+    is dropped, as util.rs:14-23 reads pairs)."""
+    x = passband_i16(o, nbits=nbits, scale=scale)
+    want = expected_text(o, x)
+    r = subprocess.run([CLI], input=x.tobytes() + tail, capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout == want, (len(r.stdout), len(want))
+
+
+@pytest.mark.gpu
+def test_demodulate_cli_panics_like_the_reference(tmp_path):
+    """Fewer than 64 samples: lock_phase's unwrap panics (exit 101); an unknown option too."""
+    r = subprocess.run([CLI], input=np.zeros(63, np.int16).tobytes(), capture_output=True, timeout=60)
+    assert r.returncode == 101 and r.stdout == b""
+    r = subprocess.run([CLI, "-x"], input=b"", capture_output=True, timeout=60)
+    assert r.returncode == 101
+    r = subprocess.run([CLI, "-b", "220"], input=np.zeros(64, np.int16).tobytes(), capture_output=True, timeout=60)
+    assert r.returncode == 0 and r.stdout == b""
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("chunks", [None, [1000, 1, 5000]])
-def test_demodulate_front_end(m, o, torch_cuda, chunks):
+def test_demodulator_mirror_bit_exact(m, o, torch_cuda, chunks):
+    """The Python mirror (rust_modem_amd.Demodulator, exact mix) on the GPU: the locked offset
+    and every (i, q) bit-identical to the oracle, in one call or in chunks, from i16 input."""
     torch = torch_cuda
-    sr, cf = 10000, 900
-    w = o.sample_freq(cf, sr)
-    # input: a BPSK passband (the modulator's real output, modulate.rs:128-133) scaled to i16
-    # and back, as `demodulate` reads i16 (demodulate.rs:29)
-    bits = o.prng_bits(77, 300)
-    y = o.tx_chain(o.new_phasor(o.BPSK, np.float32(np.pi / 4), 1.0), bits, 45, None, w, 0,
-                   out_mode=o.OUT_REAL)
-    x = np.round(y * 12000.0).astype(np.int16).astype(np.float32)
-    ht, lp = hilbert_taps(), lowpass_taps()
-    ref_i, ref_q, ref_off = o.demodulate_front(w, x, ht, lp)
-
-    xd = torch.from_numpy(x).cuda()
-    hil = m.FIRFilter(ht).process(xd)                       # analytic imag (demodulate.rs:32-34)
-    sig = torch.stack([xd, hil], dim=1).contiguous()
-    dem = m.Demodulator(m.Carrier(m.Freq(cf, sr)), lp)
-    rest = dem.lock_phase(sig)
+    x16 = passband_i16(o)
+    hil, lp = reference_tables()
+    ref_i, ref_q, ref_off = o.demodulate_front(o.sample_freq(CF, SR), x16.astype(np.float32), hil, lp)
+    xf = torch.from_numpy(x16.astype(np.float32)).cuda()
+    h = m.FIRFilter(hil).process(xf[:64])                   # the analytic imag for the lock
+    dem = m.Demodulator(m.Carrier(m.Freq(CF, SR)), lp)
+    dem.lock_phase(torch.stack([xf[:64], h], dim=1).contiguous())
     assert np.float32(dem.phase_offset).view(np.uint32) == np.float32(ref_off).view(np.uint32)
+    rest = torch.from_numpy(x16[64:].copy()).cuda()
     if chunks is None:
-        got = dem.process(rest.contiguous()).cpu().numpy()
+        got = dem.process(rest).cpu().numpy()
     else:
         parts, pos = [], 0
         for c in chunks + [rest.shape[0] - sum(chunks)]:
-            parts.append(dem.process(rest[pos:pos + c].contiguous()))
+            parts.append(dem.process(rest[pos:pos + c]))
             pos += c
         got = torch.cat(parts).cpu().numpy()
-    assert got.shape == (len(ref_i), 2)
     ref = np.stack([ref_i, ref_q], 1)
-    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+    assert got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("decim,L,dtype", [(1, 64, "f32"), (4, 129, "f32"), (45, 91, "f32"), (3, 31, "f16"),
+                                           (1, 23, "i16"), (8, 513, "i16")])
+def test_rx_exact_mix_bit_exact(m, o, torch_cuda, decim, L, dtype):
+    """MODEM_MIX_REFERENCE_REAL_EXACT at any decimation: every kept output bit-identical to
+    Demodulator's (or_demodulate at the same instants), streamed in ragged calls."""
+    torch = torch_cuda
+    rng = np.random.default_rng(decim * 1000 + L)
+    n = 40000
+    taps = (rng.standard_normal(L) * 0.1).astype(np.float32)
+    re = (rng.standard_normal(n) * 900).astype(np.float32)
+    if dtype == "i16":
+        x16 = np.round(re).astype(np.int16)
+        re = x16.astype(np.float32)
+        xin, in_dtype = torch.from_numpy(x16).cuda(), m.DTYPE_I16
+    elif dtype == "f16":
+        xh = np.stack([re / 64, rng.standard_normal(n)], 1).astype(np.float16)
+        re = xh[:, 0].astype(np.float32)
+        xin, in_dtype = torch.from_numpy(xh).cuda(), m.DTYPE_F16
+    else:
+        xin, in_dtype = torch.from_numpy(np.stack([re, rng.standard_normal(n).astype(np.float32)], 1)).cuda(), m.DTYPE_F32
+    w, s0, off = o.sample_freq(CF, SR), 12345, np.float32(0.3)
+    ri, rq = o.demodulate(w, s0, float(off), taps, re)
+    D = 7 % decim
+    keep = np.arange(D, n, decim)
+    rx = m.DemodulatorRx(m.Carrier(w, s0), taps, decim=decim, decim_offset=D, mix=m.MIX_REFERENCE_REAL_EXACT,
+                         in_dtype=in_dtype, phase_offset=float(off))
+    parts, pos = [], 0
+    for c in [1, 4095, 17, 9000, n]:
+        iq, _ = rx.process(xin[pos:pos + c], want_sym=False)
+        parts.append(iq.cpu().numpy())
+        pos += c
+        if pos >= n:
+            break
+    got = np.concatenate(parts)
+    ref = np.stack([ri[keep], rq[keep]], 1)
+    assert got.shape == ref.shape
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_fir_bit_exact(m, o, torch_cuda):
+    """modem_fir == FIRFilter::add bit for bit (the fold of fir.rs:18-34, no fusion)."""
+    rng = np.random.default_rng(11)
+    for L in (1, 23, 64, 1000):
+        taps = rng.standard_normal(L).astype(np.float32)
+        x = rng.standard_normal(20000).astype(np.float32)
+        ref = o.fir_block(taps, x)
+        f = m.FIRFilter(taps)
+        xt = torch_cuda.from_numpy(x).cuda()
+        y = np.concatenate([f.process(xt[:777]).cpu().numpy(), f.process(xt[777:]).cpu().numpy()])
+        assert np.array_equal(y.view(np.uint32), ref.view(np.uint32)), L
