@@ -73,39 +73,22 @@ __device__ __forceinline__ float carrier_phase_off(float w, uint64_t base, int o
     return phase_from_f(w, nf);
 }
 
-// sin/cos of a phase in [0, 2pi]. MODEM_PRECISE_TRIG selects a Cody-Waite + minimax
-// polynomial (<= 2 ulp); the default uses the hardware v_sin_f32/v_cos_f32 (input in
-// revolutions). Either way the sample tolerance is set in tests/test_gpu_parity.py.
+// sin/cos of a phase in [0, 2pi] on the hardware v_sin_f32/v_cos_f32 (input in revolutions);
+// the sample tolerance is set in tests/test_gpu_parity.py. (The bit-exact libm results of the
+// reference's own demodulator: libm_sincosf.h.)
 __device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
 #if defined(MODEM_ABLATE_TRIG)        // profiling builds only (tools/ablate.sh)
     s = ph; c = 1.0f;
     return;
 #endif
-#ifdef MODEM_PRECISE_TRIG
-    const float j = __builtin_rintf(ph * 0.63661977236758134f);
-    float r = __builtin_fmaf(-j, 1.57079637050628662f, ph);
-    r = __builtin_fmaf(-j, -4.37113900018624283e-8f, r);
-    const float r2 = r * r;
-    float sp = __builtin_fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
-    sp = __builtin_fmaf(r2, sp, -1.6666654611e-1f);
-    const float sr = __builtin_fmaf(r * r2, sp, r);
-    float cp = __builtin_fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
-    cp = __builtin_fmaf(r2, cp, 4.166664568298827e-2f);
-    const float cr = __builtin_fmaf(r2 * r2, cp, __builtin_fmaf(-0.5f, r2, 1.0f));
-    const int q = (int)j & 3;
-    const float ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
-    s = (q & 2) ? -ss : ss;
-    c = ((q + 1) & 2) ? -cc : cc;
-#else
     s = __sinf(ph);
     c = __cosf(ph);
-#endif
 }
 
 // Hardware sin/cos of two phases (what __sinf/__cosf compile to: v_sin/v_cos of phase/2pi,
 // here with one packed multiply for both samples).
 __device__ __forceinline__ void sincos_phase2(cf2 ph, cf2& s, cf2& c) {
-#if defined(MODEM_ABLATE_TRIG) || defined(MODEM_PRECISE_TRIG)
+#if defined(MODEM_ABLATE_TRIG)
     sincos_phase(ph.x, s.x, c.x);
     sincos_phase(ph.y, s.y, c.y);
 #else
@@ -206,12 +189,6 @@ static inline int resident_blocks(const void* kernel, int threads, size_t lds) {
     return occ;
 }
 
-// Optional cap on workgroups per CU (0 = occupancy limit), e.g. to leave room for a kernel of
-// another stream that runs concurrently (experiments: MODEM_TX_WGS_PER_CU / MODEM_RX_WGS_PER_CU).
-static inline int env_wgs_per_cu(const char* name) {
-    const char* v = std::getenv(name);
-    return v ? std::atoi(v) : 0;
-}
 
 static inline unsigned persistent_grid(const void* kernel, int threads, size_t lds, int64_t ntiles,
                                        int cap_per_cu = 0) {

@@ -460,12 +460,6 @@ __device__ __forceinline__ uint8_t rx_slice_qam2(const RxParams& p, float re, fl
 // wave votes with three ballots whether the tile's max lies in that exponent's window. A tile
 // outside it, and the call's first tile (its window reads the history), take the general
 // path: per-sample loads, two passes, the same tile_ka -> identical results either way.
-#ifndef RXLD_AUX
-#define RXLD_AUX 0
-#endif
-#ifndef RXST_AUX
-#define RXST_AUX 0
-#endif
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
 struct RxMfma {
     using Q = Quad<InT>;
@@ -563,11 +557,11 @@ struct RxMfma {
         constexpr int S = sizeof(InT) * 2;
         const int o = voff + 4 * NT * u * S;
         if constexpr (std::is_same<InT, float>::value) {
-            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, RXLD_AUX));
-            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, RXLD_AUX));
+            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, 0));
             return QT{make_float4(a[0], a[1], a[2], a[3]), make_float4(b[0], b[1], b[2], b[3])};
         } else {
-            return __builtin_bit_cast(QT, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, RXLD_AUX));
+            return __builtin_bit_cast(QT, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
         }
     }
 
@@ -712,14 +706,14 @@ struct RxMfma {
             const float a = re[r] * GAIN, b = im[r] * GAIN;
             if (EM & RXE_IQ) {
                 if constexpr (std::is_same<OutT, float>::value)
-                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(a, b)), riq, 8 * off, 0, RXST_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(a, b)), riq, 8 * off, 0, 0);
                 else
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, __floats2half2_rn(a, b)), riq, 4 * off, 0, RXST_AUX);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, __floats2half2_rn(a, b)), riq, 4 * off, 0, 0);
             }
             if (EM & RXE_SYM) {
                 const uint8_t sy = !(EM & RXE_NEAREST) ? rx_slice_qam2(p, a, b)
                                  : p.bps == 2 ? rx_slice_nearest4(p, a, b) : rx_slice_nearest(p, a, b);
-                __builtin_amdgcn_raw_buffer_store_b8(sy, rsy, off, 0, RXST_AUX);
+                __builtin_amdgcn_raw_buffer_store_b8(sy, rsy, off, 0, 0);
             }
         }
     }

@@ -447,12 +447,6 @@ struct TxMfma {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             char* q = ob + (uint32_t)((loff + 16 * r) * SBYTES);
-#ifdef MODEM_TX_NT_STORE
-            if (OUT_MODE != OUT_REAL && std::is_same<OutT, float>::value) {
-                __builtin_nontemporal_store(z[r], reinterpret_cast<cf2*>(q));
-                continue;
-            }
-#endif
             if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(q, 0, z[r].x);
             else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
         }
@@ -590,13 +584,8 @@ __global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __re
 // b serves channel b / g as its workgroup b % g of g.
 template <int SPS, int NKS, int OUT_MODE, typename OutT>
 __global__ __launch_bounds__(256) void tx_mfma_batch(const TxBatch b, const th8* __restrict__ bfrag) {
-#ifdef MODEM_BATCH_INTERLEAVE
-    const int ch = (int)(blockIdx.x % (unsigned)b.nch);
-    const unsigned bid = blockIdx.x / (unsigned)b.nch;
-#else
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
     const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
-#endif
     const TxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
     tx_mfma_body<SPS, NKS, OUT_MODE, OutT>(p, bfrag, bid, b.g);
 }
@@ -814,8 +803,7 @@ static hipError_t txm_go(const TxParams& p, const void* bfrag, hipStream_t s) {
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
     const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << p.bps) * 8;
     const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT>);
-    static const int cap = env_wgs_per_cu("MODEM_TX_WGS_PER_CU");
-    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT>), dim3(persistent_grid(k, K::NT, lds, ntiles, cap)),
+    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
                        dim3(K::NT), lds, s, p, static_cast<const th8*>(bfrag));
     return hipGetLastError();
 }
