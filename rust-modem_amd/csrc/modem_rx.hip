@@ -460,12 +460,14 @@ __device__ __forceinline__ uint8_t rx_slice_qam2(const RxParams& p, float re, fl
 // wave votes with three ballots whether the tile's max lies in that exponent's window. A tile
 // outside it, and the call's first tile (its window reads the history), take the general
 // path: per-sample loads, two passes, the same tile_ka -> identical results either way.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF_ = 4>
 struct RxMfma {
     using Q = Quad<InT>;
     using QT = typename Q::T;
-    static constexpr int NT = 256;                              // 4 waves
-    static constexpr int TS = 1024;                             // kept instants per tile
+    static constexpr int NT = 256;                              // 4 waves stage every tile
+    static constexpr int NW = NT / 64;
+    static constexpr int NWF = NWF_;                            // of which NWF filter it: 4, or 1 (small calls)
+    static constexpr int TS = NWF * 256;                        // kept instants per tile
     static constexpr int RW = 16 * DEC;                         // samples per A row
     static constexpr int W = 32 * NKS;
     static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
@@ -474,7 +476,7 @@ struct RxMfma {
     // Plane layout. decim 4: unpadded, 16-B chunks XOR-swizzled within each aligned group of
     // 8 chunks — conflict-free A reads (tests/test_lds_banks.py) and 4 KiB less LDS per
     // workgroup than padding, which lets 4 workgroups share a CU. Otherwise rxh_pos.
-    static constexpr bool SWZ = DEC == 4;
+    static constexpr bool SWZ = DEC == 4 && NT == 256;
     __host__ __device__ static constexpr int ppos(int e) {
         return SWZ ? ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7)) : rxh_pos(e, RW);
     }
@@ -533,13 +535,17 @@ struct RxMfma {
     // After the barrier: do the waves' votes put the staged tile inside the window of k?
     // (k == 0 also accepts an all-zero / subnormal tile, whose tile_ka is 0.)
     __device__ static bool fast_ok(const int* votes, int k) {
-        const int f = votes[0] | votes[1] | votes[2] | votes[3];
+        int f = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) f |= votes[w];
         const bool good = k == 0 ? !(f & 2) && ((f & 1) || !(f & 4)) : (f & 1) && !(f & 2);
         return __builtin_amdgcn_readfirstlane((int)good) != 0;
     }
     __device__ static int read_ka(const float* r) {
-        return __builtin_amdgcn_readfirstlane(tile_ka(f32_exp(
-            __builtin_fmaxf(__builtin_fmaxf(r[0], r[1]), __builtin_fmaxf(r[2], r[3])))));
+        float m = r[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) m = __builtin_fmaxf(m, r[w]);
+        return __builtin_amdgcn_readfirstlane(tile_ka(f32_exp(m)));
     }
 
     // Staging slot u of a tile through a buffer descriptor whose base is the tile window's
@@ -677,8 +683,9 @@ struct RxMfma {
     }
 
     // D[row][col]: row = 4*(lane>>4) + r, col = lane&15 -> instant ot + 16*row + col. Stores
-    // through buffer descriptors sized to the instants still in the call (a call's last tile
-    // computes past them).
+    // through buffer descriptors over the wave's instants that are in the call: those before
+    // the call's first (ot < 0: a lane offset below the base wraps out of range) and past its
+    // last are dropped without a branch.
     template <int EM>
     __device__ static void emit(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
         const int lane = tid_() & 63;
@@ -686,15 +693,17 @@ struct RxMfma {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t o = ot + 16 * (4 * (lane >> 4) + r) + (lane & 15);
-                if (o < p.nout)
+                if (o >= 0 && o < p.nout)
                     rx_emit<OutT>(p, o, GAIN * __builtin_ldexpf(dre[r], -kab), GAIN * __builtin_ldexpf(dim[r], -kab));
             }
             return;
         }
-        const int64_t left = p.nout - ot;
+        const int64_t ob = ot < 0 ? 0 : ot;
+        const int sh = (int)(ot - ob);                       // -15 .. 0
+        const int64_t left = p.nout - ob;
         const uint32_t nk = left < 256 ? (uint32_t)(left > 0 ? left : 0) : 256u;
-        const __amdgpu_buffer_rsrc_t riq = buf_rsrc(reinterpret_cast<OutT*>(p.out_iq) + 2 * ot, nk * 2 * sizeof(OutT));
-        const __amdgpu_buffer_rsrc_t rsy = buf_rsrc(p.out_sym + ot, nk);
+        const __amdgpu_buffer_rsrc_t riq = buf_rsrc(reinterpret_cast<OutT*>(p.out_iq) + 2 * ob, nk * 2 * sizeof(OutT));
+        const __amdgpu_buffer_rsrc_t rsy = buf_rsrc(p.out_sym + ob, nk);
         f32x4 re = dre, im = dim;
         if (kab != 0) {                        // uniform
 #pragma unroll
@@ -702,7 +711,7 @@ struct RxMfma {
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const uint32_t off = (uint32_t)(16 * (4 * (lane >> 4) + r) + (lane & 15));
+            const uint32_t off = (uint32_t)(16 * (4 * (lane >> 4) + r) + (lane & 15) + sh);
             const float a = re[r] * GAIN, b = im[r] * GAIN;
             if (EM & RXE_IQ) {
                 if constexpr (std::is_same<OutT, float>::value)
@@ -720,6 +729,7 @@ struct RxMfma {
 
     // General path for tile t (all waves): two passes over its samples (max, then tile_ka
     // scale + split), the matched filter, the outputs in range. Returns its tile_ka.
+    template <int EM>
     __device__ static int slow_tile(const RxParams& p, _Float16* pl, const _Float16* tbl, float* reds, int64_t t,
                                     int kb, int ld) {
         // lane values recomputed here, not hoisted to the kernel entry (where, live across
@@ -727,36 +737,77 @@ struct RxMfma {
         const int tid = tid_();
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int64_t q_lo = q_lo_of(p, t), n_lo = q_lo + p.n_start;
+        // 1. The window's raw samples into the planes' LDS (free until this tile is staged),
+        //    each through two buffer descriptors, one over the chunk and one over the history
+        //    (only a call's first tile reaches before the chunk): out of range loads return
+        //    zeros without a memory access, so the loads carry no branches and are all in
+        //    flight together.
+        float2* raw = reinterpret_cast<float2*>(pl);
+        {
+            constexpr int S = sizeof(InT) * 2;
+            const int64_t ex = q_lo >= 0 ? 0 : -q_lo;                 // first window sample in the chunk
+            const int64_t qx = q_lo + ex;
+            const int64_t nx = p.N - qx < NS ? p.N - qx : NS;
+            const __amdgpu_buffer_rsrc_t rx = buf_rsrc(reinterpret_cast<const char*>(p.x) + qx * S,
+                                                       (uint32_t)(nx > 0 ? nx : 0) * S);
+            const int64_t hb = q_lo + p.HL;                           // history index of sample 0
+            const int64_t eh = hb >= 0 ? 0 : -hb;                     // first window sample in the history
+            const int64_t nhist = p.HL - (hb + eh);
+            const __amdgpu_buffer_rsrc_t rh = buf_rsrc(reinterpret_cast<const char*>(p.hist) + (hb + eh) * S,
+                                                       (uint32_t)(nhist > 0 ? nhist : 0) * S);
+            const int ox = (int)ex, oh = (int)eh;
+#pragma unroll
+            for (int k = 0; k < (NS + NT - 1) / NT; ++k) {
+                const int e = tid + k * NT;
+                if ((k + 1) * NT > NS && e >= NS) break;
+                const uint32_t fx = (uint32_t)(e - ox) * S, fh = (uint32_t)(e - oh) * S;   // < 0: wraps, out of range
+                float2 v, w;
+                if constexpr (std::is_same<InT, float>::value) {
+                    v = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, fx, 0, 0));
+                    w = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, fh, 0, 0));
+                } else {
+                    v = __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(rx, fx, 0, 0)));
+                    w = __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(rh, fh, 0, 0)));
+                }
+                raw[e] = e >= ox ? v : w;
+            }
+        }
+        __syncthreads();
+        // 2. Mix (rx_mix: the same values as the fast path's), the tile's max.
+        float zr[U][4], zi[U][4];
         float mx = 0.f;
-        for (int e0 = 4 * tid; e0 < NS; e0 += 4 * NT)
-            for (int j = 0; j < 4 && e0 + j < NS; ++j) {
-                const float2 z = rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e0 = 4 * (tid + NT * u);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float2 z = make_float2(0.f, 0.f);
+                if (e0 + j < NS) z = rx_mix<MIX>(p, n_lo, e0 + j, raw[e0 + j]);
+                zr[u][j] = z.x;
+                zi[u][j] = z.y;
                 mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(z.x), __builtin_fabsf(z.y)));
             }
+        }
         mx = wave_max(mx);
         if ((tid & 63) == 0) reds[wave] = mx;
-        __syncthreads();
+        __syncthreads();                       // also: every raw read done before the planes overwrite it
+        // 3. Scale by 2^tile_ka, split, stage.
         const int ka = read_ka(reds);
         const float sc = __builtin_ldexpf(1.0f, ka);
-        for (int e0 = 4 * tid; e0 < NS; e0 += 4 * NT) {
-            float zr[4], zi[4];
-            for (int j = 0; j < 4; ++j) {
-                const float2 z = e0 + j < NS ? rx_mix<MIX>(p, n_lo, e0 + j, rx_sample<InT>(p, q_lo + e0 + j))
-                                             : make_float2(0.f, 0.f);
-                zr[j] = z.x * sc;
-                zi[j] = z.y * sc;
-            }
-            put4(pl, ppos(e0), zr, zi);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e0 = 4 * (tid + NT * u);
+            if (e0 >= NS) continue;
+            float a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { a[j] = zr[u][j] * sc; b[j] = zi[u][j] * sc; }
+            put4(pl, ppos(e0), a, b);
         }
         __syncthreads();
         f32x4 dre, dim;
-        fir(pl, tbl, dre, dim);
-        const int64_t ot = t * TS + wave * 256 - ld;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t o = ot + 16 * (4 * ((tid & 63) >> 4) + r) + (tid & 15);
-            if (o >= 0 && o < p.nout)
-                rx_emit<OutT>(p, o, GAIN * __builtin_ldexpf(dre[r], -(ka + kb)), GAIN * __builtin_ldexpf(dim[r], -(ka + kb)));
+        if (wave < NWF) {                      // uniform
+            fir(pl, tbl, dre, dim);
+            emit<EM>(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
         }
         __syncthreads();                       // the planes are restaged next
         return ka;
@@ -793,8 +844,10 @@ struct RxMfma {
             __syncthreads();
             if (!(fi && fast_ok(votes, kpred))) return;
             f32x4 dre, dim;
-            fir(pl, tbl, dre, dim);
-            emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
+            if (NWF == NW || wave < NWF) {     // uniform
+                fir(pl, tbl, dre, dim);
+                emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
+            }
             __syncthreads();                   // the planes are restaged next
             ++i;
         }
@@ -841,7 +894,7 @@ struct RxMfma {
             if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
             else loop<true, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
             if (i < sq.count) {                // tile i on the general path (one place in the code)
-                kpred = slow_tile(p, pl, tbl, reds, sq.first + i * sq.step, cx.kb, cx.ld);
+                kpred = slow_tile<EM>(p, pl, tbl, reds, sq.first + i * sq.step, cx.kb, cx.ld);
                 ++i;
                 // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
                 // not held across the general path, which has no registers to spare)
@@ -855,10 +908,10 @@ struct RxMfma {
 
 // One channel's share of a launch: workgroup `bid` of `nb` working on channel p, with the
 // epilogue EM chosen on the host (rx_mfma_em): each kernel keeps only its own stores.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
 __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* __restrict__ tables, int64_t bid,
                                              int64_t nb) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
     _Float16* pl = lds_h;                                   // 4 sample planes
     _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
@@ -881,21 +934,21 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     K::template run<EM>(p, pl, tbl, red, sq, bid);
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT>::WPE)))
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NWF>::WPE)))
 void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, EM>(p, tables, blockIdx.x, gridDim.x);
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM>(p, tables, blockIdx.x, gridDim.x);
 }
 
 // A batch of independent channels of one configuration (modem_rx_process_batch): workgroup
 // b serves channel b / g as its workgroup b % g of g.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT>::WPE)))
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NWF>::WPE)))
 void rx_mfma_batch(const RxBatch b, const _Float16* __restrict__ tables) {
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
     const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
     const RxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, EM>(p, tables, bid, b.g);
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM>(p, tables, bid, b.g);
 }
 
 // The epilogue specialisation for a call: stores known at compile time for the loopback
@@ -1028,43 +1081,54 @@ static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s
                                      : rx_dec<InT, MIX_COMPLEX, OutT>(p, decim, s);
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+// Tile size by the work: 1024-instant tiles (4 filter waves) when the call has at least four
+// per CU, else 256-instant tiles staged by 4 waves and filtered by one, so that a small call
+// (C2: 2^18 instants) still spreads its staging over every SIMD. The filter of a 16-instant
+// row is the same code either way: results do not depend on the choice.
+inline bool rx_small_tiles(int64_t ninst) { return ninst < (int64_t)4 * 1024 * device_cus(); }
+
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
 static hipError_t rxm_go_em(const RxParams& p, const void* tables, hipStream_t s) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
     const int64_t ntiles = (p.nout + (p.k_first & 15) + K::TS - 1) / K::TS;
-    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, EM>);
-    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, EM>), dim3(persistent_grid(k, K::NT, K::LDS_BYTES, ntiles)),
+    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM>);
+    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM>), dim3(persistent_grid(k, K::NT, K::LDS_BYTES, ntiles)),
                        dim3(K::NT), K::LDS_BYTES, s, p, static_cast<const _Float16*>(tables));
     return hipGetLastError();
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int EM>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
 static hipError_t rxm_go_batch_em(RxBatch b, const void* tables, hipStream_t s) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT>;
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
     int64_t ntiles = 0;
     for (int c = 0; c < b.nch; ++c) {
         const int64_t t = (b.p[c].nout + (b.p[c].k_first & 15) + K::TS - 1) / K::TS;
         ntiles = t > ntiles ? t : ntiles;
     }
-    const void* k = reinterpret_cast<const void*>(&rx_mfma_batch<DEC, NKS, InT, MIX, OutT, EM>);
+    const void* k = reinterpret_cast<const void*>(&rx_mfma_batch<DEC, NKS, InT, MIX, OutT, NWF, EM>);
     const int64_t cap = persistent_grid(k, K::NT, K::LDS_BYTES, INT64_MAX);
     int64_t g = cap / b.nch;
     g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
     b.g = (int32_t)g;
-    hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX, OutT, EM>), dim3((unsigned)(g * b.nch)),
+    hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX, OutT, NWF, EM>), dim3((unsigned)(g * b.nch)),
                        dim3(K::NT), K::LDS_BYTES, s, b, static_cast<const _Float16*>(tables));
     return hipGetLastError();
 }
 
-// Dispatch on the epilogue: the specialised ones exist only where rx_mfma_em can pick them.
+// Dispatch on the epilogue (the specialised ones exist only where rx_mfma_em can pick them)
+// and on the tile size.
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, bool BATCH, typename Arg>
-static hipError_t rxm_em(const Arg& a, int em, const void* tables, hipStream_t s) {
+static hipError_t rxm_em(const Arg& a, int em, bool small, const void* tables, hipStream_t s) {
     constexpr bool loop = std::is_same<InT, OutT>::value && MIX == MIX_COMPLEX;
     constexpr bool f32 = std::is_same<InT, float>::value;
     auto go = [&](auto emc) {
         constexpr int E = decltype(emc)::value;
-        if constexpr (BATCH) return rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, E>(a, tables, s);
-        else return rxm_go_em<DEC, NKS, InT, MIX, OutT, E>(a, tables, s);
+        if constexpr (BATCH)
+            return small ? rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, 1, E>(a, tables, s)
+                         : rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, 4, E>(a, tables, s);
+        else
+            return small ? rxm_go_em<DEC, NKS, InT, MIX, OutT, 1, E>(a, tables, s)
+                         : rxm_go_em<DEC, NKS, InT, MIX, OutT, 4, E>(a, tables, s);
     };
     switch (em) {
     case RXE_IQSYM: return go(std::integral_constant<int, loop ? RXE_IQSYM : RXE_GEN>());
@@ -1077,20 +1141,24 @@ static hipError_t rxm_em(const Arg& a, int em, const void* tables, hipStream_t s
 
 template <int DEC, int NKS, typename InT, int MIX, typename OutT>
 static hipError_t rxm_go(const RxParams& p, const void* tables, hipStream_t s) {
-    return rxm_em<DEC, NKS, InT, MIX, OutT, false>(p, rx_mfma_em<InT, MIX, OutT>(p), tables, s);
+    return rxm_em<DEC, NKS, InT, MIX, OutT, false>(p, rx_mfma_em<InT, MIX, OutT>(p), rx_small_tiles(p.nout),
+                                                   tables, s);
 }
 
 template <int DEC, int NKS, typename InT, typename OutT>
 static hipError_t rxm_go_batch(const RxBatch& b, const void* tables, hipStream_t s) {
     int em = rx_mfma_em<InT, MIX_COMPLEX, OutT>(b.p[0]);          // one epilogue for the batch
-    for (int c = 1; c < b.nch; ++c)
+    int64_t ninst = 0;
+    for (int c = 0; c < b.nch; ++c) {
         if (rx_mfma_em<InT, MIX_COMPLEX, OutT>(b.p[c]) != em) em = RXE_GEN;
-    return rxm_em<DEC, NKS, InT, MIX_COMPLEX, OutT, true>(b, em, tables, s);
+        ninst += b.p[c].nout;
+    }
+    return rxm_em<DEC, NKS, InT, MIX_COMPLEX, OutT, true>(b, em, rx_small_tiles(ninst), tables, s);
 }
 
 // (decim, k-steps) variants: W = 32 * nks >= 15 * decim + ntaps.
-#ifdef MODEM_DEV_MIN      // experiment builds: the C3 variant only
-#define RXM_TABLE(X) X(4, 6)
+#ifdef MODEM_DEV_MIN      // experiment builds: the C2 and C3 variants only
+#define RXM_TABLE(X) X(4, 4) X(4, 6)            // C2, C3
 #else
 #define RXM_TABLE(X) X(2, 2) X(2, 3) X(2, 5) X(2, 8) X(4, 3) X(4, 4) X(4, 6) X(4, 8) X(8, 5) X(8, 6) X(8, 9) X(8, 20)
 #endif

@@ -278,10 +278,10 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
 // (lead = symbols before this call, mod SB), so a symbol always meets the same taps at the
 // same k positions and a stream cut into calls gives the same samples as one call.
 // Sample-and-hold (no taps) stays on the exact VALU kernels.
-template <int SPS> struct TxMfmaCfg {
+template <int SPS, int SUB_> struct TxMfmaCfg {
     static constexpr int SB = 16 / SPS;          // symbols per row-block
     static constexpr int NT = 256;               // 4 waves
-    static constexpr int SUB = 4;                // 16x16 tiles per wave per tile
+    static constexpr int SUB = SUB_;             // 16x16 tiles per wave per tile: 4, 1 (small calls)
     static constexpr int TS = 4 * SUB * 16 * SB; // symbols per workgroup tile
     static constexpr int NCOP = SB % 4 == 0 ? 1 : 4 / SB;   // plane copies (8-B aligned A reads)
 };
@@ -298,9 +298,9 @@ __device__ __forceinline__ cf2 tx_cmix(cf2 y, cf2 cssn) {
 typedef _Float16 th8 __attribute__((ext_vector_type(8)));
 typedef _Float16 th4 __attribute__((ext_vector_type(4)));
 
-template <int SPS, int NKS, int OUT_MODE, typename OutT>
+template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB_ = 4>
 struct TxMfma {
-    using C = TxMfmaCfg<SPS>;
+    using C = TxMfmaCfg<SPS, SUB_>;
     static constexpr int SB = C::SB, NT = C::NT, SUB = C::SUB, TS = C::TS, NCOP = C::NCOP;
     static constexpr int W = 32 * NKS;             // window symbols per row-block
     static constexpr int PRE = W - SB;             // window symbols before a row-block
@@ -541,10 +541,10 @@ struct TxMfma {
 };
 
 // One channel's share of a launch: workgroup `bid` of `nb` working on channel p.
-template <int SPS, int NKS, int OUT_MODE, typename OutT>
+template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
 __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __restrict__ bfrag,
                                              int64_t bid, int64_t nb) {
-    using K = TxMfma<SPS, NKS, OUT_MODE, OutT>;
+    using K = TxMfma<SPS, NKS, OUT_MODE, OutT, SUB>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_t[];
     _Float16* pl = lds_t;
     th4* lut_s = reinterpret_cast<th4*>(lds_t + K::PLANES);
@@ -575,19 +575,19 @@ __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __res
     K::template run<0>(p, pl, lut_s, bh, bl, t0, t1, ts);
 }
 
-template <int SPS, int NKS, int OUT_MODE, typename OutT>
+template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
 __global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
-    tx_mfma_body<SPS, NKS, OUT_MODE, OutT>(p, bfrag, blockIdx.x, gridDim.x);
+    tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, blockIdx.x, gridDim.x);
 }
 
 // A batch of independent channels of one configuration (modem_tx_process_batch): workgroup
 // b serves channel b / g as its workgroup b % g of g.
-template <int SPS, int NKS, int OUT_MODE, typename OutT>
+template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
 __global__ __launch_bounds__(256) void tx_mfma_batch(const TxBatch b, const th8* __restrict__ bfrag) {
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
     const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
     const TxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
-    tx_mfma_body<SPS, NKS, OUT_MODE, OutT>(p, bfrag, bid, b.g);
+    tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, bid, b.g);
 }
 
 // Any samples-per-symbol: thread per output sample, symbols staged in LDS.
@@ -797,41 +797,55 @@ static hipError_t tx_mode(const TxParams& p, int sps, int out_mode, hipStream_t 
     }
 }
 
-template <int SPS, int NKS, int OM, typename OutT>
-static hipError_t txm_go(const TxParams& p, const void* bfrag, hipStream_t s) {
-    using K = TxMfma<SPS, NKS, OM, OutT>;
+// Tile size by the work: 4 sub-tiles per wave when the call has at least four such tiles
+// per CU, else one (a small call, C2: 2^18 symbols, then still spreads over every SIMD). The
+// 16x16 sub-tiles are computed alike either way: results do not depend on the choice.
+inline bool tx_small_tiles(int64_t nsym, int sb) { return nsym < (int64_t)4 * 4 * 4 * 16 * sb * device_cus(); }
+
+template <int SPS, int NKS, int OM, typename OutT, int SUB>
+static hipError_t txm_go_sub(const TxParams& p, const void* bfrag, hipStream_t s) {
+    using K = TxMfma<SPS, NKS, OM, OutT, SUB>;
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
     const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << p.bps) * 8;
-    const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT>);
-    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
+    const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT, SUB>);
+    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT, SUB>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
                        dim3(K::NT), lds, s, p, static_cast<const th8*>(bfrag));
     return hipGetLastError();
 }
-
-// Batch: g workgroups per channel, the persistent grid shared out over the channels (at least
-// one workgroup each, never more than the channel with the most tiles can use).
 template <int SPS, int NKS, int OM, typename OutT>
-static hipError_t txm_go_batch(TxBatch b, const void* bfrag, hipStream_t s) {
-    using K = TxMfma<SPS, NKS, OM, OutT>;
+static hipError_t txm_go(const TxParams& p, const void* bfrag, hipStream_t s) {
+    return tx_small_tiles(p.nsym, 16 / SPS) ? txm_go_sub<SPS, NKS, OM, OutT, 1>(p, bfrag, s)
+                                            : txm_go_sub<SPS, NKS, OM, OutT, 4>(p, bfrag, s);
+}
+template <int SPS, int NKS, int OM, typename OutT, int SUB>
+static hipError_t txm_go_batch_sub(TxBatch b, const void* bfrag, hipStream_t s) {
+    using K = TxMfma<SPS, NKS, OM, OutT, SUB>;
     int64_t ntiles = 0;
     for (int c = 0; c < b.nch; ++c) {
         const int64_t t = (b.p[c].nsym + b.p[c].lead + K::TS - 1) / K::TS;
         ntiles = t > ntiles ? t : ntiles;
     }
     const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << b.p[0].bps) * 8;
-    const void* k = reinterpret_cast<const void*>(&tx_mfma_batch<SPS, NKS, OM, OutT>);
+    const void* k = reinterpret_cast<const void*>(&tx_mfma_batch<SPS, NKS, OM, OutT, SUB>);
     const int64_t cap = persistent_grid(k, K::NT, lds, INT64_MAX);
     int64_t g = cap / b.nch;
     g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
     b.g = (int32_t)g;
-    hipLaunchKernelGGL((tx_mfma_batch<SPS, NKS, OM, OutT>), dim3((unsigned)(g * b.nch)), dim3(K::NT), lds, s, b,
+    hipLaunchKernelGGL((tx_mfma_batch<SPS, NKS, OM, OutT, SUB>), dim3((unsigned)(g * b.nch)), dim3(K::NT), lds, s, b,
                        static_cast<const th8*>(bfrag));
     return hipGetLastError();
 }
+template <int SPS, int NKS, int OM, typename OutT>
+static hipError_t txm_go_batch(TxBatch b, const void* bfrag, hipStream_t s) {
+    int64_t nsym = 0;
+    for (int c = 0; c < b.nch; ++c) nsym += b.p[c].nsym;
+    return tx_small_tiles(nsym, 16 / SPS) ? txm_go_batch_sub<SPS, NKS, OM, OutT, 1>(b, bfrag, s)
+                                          : txm_go_batch_sub<SPS, NKS, OM, OutT, 4>(b, bfrag, s);
+}
 
 // (sps, k-steps) variants: W = 32 * nks >= 16/sps + K - 1 symbols (K = taps per phase).
-#ifdef MODEM_DEV_MIN      // experiment builds: the C3 variant only
-#define TXM_TABLE(X) X(4, 2)
+#ifdef MODEM_DEV_MIN      // experiment builds: the C2 and C3 variants only
+#define TXM_TABLE(X) X(4, 1) X(4, 2)            // C2, C3
 #else
 #define TXM_TABLE(X) X(2, 1) X(2, 2) X(2, 3) X(2, 5) X(4, 1) X(4, 2) X(4, 3) X(4, 5) X(4, 9) \
                      X(8, 1) X(8, 2) X(8, 3) X(8, 5) X(8, 9) X(16, 1) X(16, 2) X(16, 3) X(16, 5)
