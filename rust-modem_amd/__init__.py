@@ -480,15 +480,28 @@ def _is_torch(x) -> bool:
     return type(x).__module__.startswith("torch")
 
 
+_TORCH = None
+
+
+def _torch_cuda():
+    """torch when it has a GPU, else False (looked up once: is_available() costs ~1 us)."""
+    global _TORCH
+    if _TORCH is None:
+        try:
+            import torch
+            _TORCH = torch if torch.cuda.is_available() else False
+        except ImportError:
+            _TORCH = False
+    return _TORCH
+
+
 def _stream_handle(stream) -> Optional[int]:
     if stream is not None:
         return int(getattr(stream, "cuda_stream", stream))
-    try:
-        import torch
-        if torch.cuda.is_available():
-            return int(torch.cuda.current_stream().cuda_stream)
-    except ImportError:
-        pass
+    t = _torch_cuda()
+    if t:
+        # the current stream's raw handle (current_stream() builds a Stream object: ~3 us)
+        return t._C._cuda_getCurrentRawStream(t._C._cuda_getDevice())
     return None
 
 
@@ -582,8 +595,8 @@ class DigitalModulator:
                                                ctypes.byref(prod), _stream_handle(stream)),
                "DigitalModulator.process")
         self._ncarry = (self._ncarry + n) % self.bps
-        self.carrier.sample = int(load_library().modem_tx_sample(self._h))
-        return out[: prod.value]
+        self.carrier.sample += prod.value        # = modem_tx_sample(h): one sample per output
+        return out if prod.value == cap else out[: prod.value]
 
     @staticmethod
     def process_batch(mods, bits, outs=None, stream=None):
@@ -714,8 +727,10 @@ class DemodulatorRx:
                                                ctypes.byref(prod), _stream_handle(stream)),
                "Demodulator.process")
         self._consumed += n
-        self.carrier.sample = int(load_library().modem_rx_sample(self._h))
-        return (None if oiq is None else oiq[: prod.value]), (None if osym is None else osym[: prod.value])
+        self.carrier.sample += n                 # = modem_rx_sample(h): one per input sample
+        k = prod.value
+        return (None if oiq is None else (oiq if int(oiq.shape[0]) == k else oiq[:k])), \
+               (None if osym is None else (osym if int(osym.shape[0]) == k else osym[:k]))
 
     @staticmethod
     def process_batch(rxs, iqs, out_iq=None, out_sym=None, stream=None):

@@ -23,15 +23,17 @@ namespace {
 
 constexpr float kPi = 3.14159265358979323846f;   // std::f32::consts::PI
 
-struct DeviceGuard {   // scoped hipSetDevice
+struct DeviceGuard {   // scoped hipSetDevice (no call when the device is already current)
     int old = -1;
-    bool ok = false;
+    bool ok = false, set = false;
     explicit DeviceGuard(int dev) {
         if (hipGetDevice(&old) != hipSuccess) { (void)hipGetLastError(); old = -1; }
+        if (old == dev) { ok = true; return; }
         ok = hipSetDevice(dev) == hipSuccess;
+        set = ok;
         if (!ok) (void)hipGetLastError();
     }
-    ~DeviceGuard() { if (old >= 0) (void)hipSetDevice(old); }
+    ~DeviceGuard() { if (set && old >= 0) (void)hipSetDevice(old); }
 };
 
 bool is_device_ptr(const void* p) {
@@ -49,6 +51,19 @@ bool foreign_ptr(const void* p, int dev) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
     return a.type == hipMemoryTypeDevice && a.device != dev;
+}
+
+// Both facts from one attribute query (the per-call host cost of a process() is mostly these
+// queries): host memory (staged), device memory the handle's kernels can use, or another
+// GPU's memory (refused).
+enum PtrKind { PTR_HOST = 0, PTR_DEVICE = 1, PTR_FOREIGN = 2 };
+PtrKind ptr_kind(const void* p, int dev) {
+    if (!p) return PTR_HOST;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return PTR_HOST; }
+    if (a.type == hipMemoryTypeManaged) return PTR_DEVICE;
+    if (a.type != hipMemoryTypeDevice) return PTR_HOST;
+    return a.device == dev ? PTR_DEVICE : PTR_FOREIGN;
 }
 
 #define HIP_TRY(expr)                                                              \
@@ -597,18 +612,19 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
     const size_t nsamp = (size_t)nsym * h->sps;
     if (nsamp > cap) return MODEM_ERR_CAPACITY;
     if (nsamp && !out) return MODEM_ERR_INVALID_ARG;
-    if ((nbits && foreign_ptr(bits, h->device)) || (nsamp && foreign_ptr(out, h->device)))
-        return MODEM_ERR_INVALID_ARG;
+    const PtrKind kb = nbits ? ptr_kind(bits, h->device) : PTR_DEVICE;
+    const PtrKind ko = nsamp ? ptr_kind(out, h->device) : PTR_DEVICE;
+    if (kb == PTR_FOREIGN || ko == PTR_FOREIGN) return MODEM_ERR_INVALID_ARG;
     DeviceGuard g(h->device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     modem_status st;
     const uint8_t* dbits = bits;
-    if (nbits && !is_device_ptr(bits)) {
+    if (kb == PTR_HOST) {
         if ((st = h->bits_stage.ensure(nbits))) return st;
         HIP_TRY(hipMemcpyAsync(h->bits_stage.p, bits, nbits, hipMemcpyHostToDevice, s));
         dbits = static_cast<const uint8_t*>(h->bits_stage.p);
     }
-    const bool host_out = nsamp && !is_device_ptr(out);
+    const bool host_out = ko == PTR_HOST;
     void* dout = out;
     if (host_out) {
         if ((st = h->out_stage.ensure(nsamp * tx_sample_bytes(h)))) return st;
@@ -903,20 +919,21 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
     int64_t k_first, nout;
     rx_range(h->consumed, h->consumed + (int64_t)n, h->decim, h->D, &k_first, &nout);
     if ((size_t)nout > cap) return MODEM_ERR_CAPACITY;
-    if ((n && !zeros && foreign_ptr(in, h->device)) || (nout && foreign_ptr(out_iq, h->device)) ||
-        (nout && foreign_ptr(out_sym, h->device)))
-        return MODEM_ERR_INVALID_ARG;
+    const PtrKind ki = n && !zeros ? ptr_kind(in, h->device) : PTR_DEVICE;
+    const PtrKind kq = nout && out_iq ? ptr_kind(out_iq, h->device) : PTR_DEVICE;
+    const PtrKind ks = nout && out_sym ? ptr_kind(out_sym, h->device) : PTR_DEVICE;
+    if (ki == PTR_FOREIGN || kq == PTR_FOREIGN || ks == PTR_FOREIGN) return MODEM_ERR_INVALID_ARG;
     DeviceGuard g(h->device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     modem_status st;
     const void* din = zeros ? h->d_zeros : in;
-    if (n && !zeros && !is_device_ptr(in)) {
+    if (ki == PTR_HOST) {
         if ((st = h->in_stage.ensure(n * rx_in_bytes(h)))) return st;
         HIP_TRY(hipMemcpyAsync(h->in_stage.p, in, n * rx_in_bytes(h), hipMemcpyHostToDevice, s));
         din = h->in_stage.p;
     }
-    const bool host_iq = nout && out_iq && !is_device_ptr(out_iq);
-    const bool host_sym = nout && out_sym && !is_device_ptr(out_sym);
+    const bool host_iq = kq == PTR_HOST;
+    const bool host_sym = ks == PTR_HOST;
     void* diq = out_iq;
     uint8_t* dsym = out_sym;
     if (host_iq) {
@@ -1051,19 +1068,20 @@ modem_status modem_fir_create(const float* taps, uint32_t ntaps, int device, mod
 
 modem_status modem_fir_process(modem_fir* h, const float* in, float* out, size_t n, void* stream) {
     if (!h || (n && (!in || !out))) return MODEM_ERR_INVALID_ARG;
-    if (n && (foreign_ptr(in, h->device) || foreign_ptr(out, h->device))) return MODEM_ERR_INVALID_ARG;
+    const PtrKind ki = n ? ptr_kind(in, h->device) : PTR_DEVICE, ko = n ? ptr_kind(out, h->device) : PTR_DEVICE;
+    if (ki == PTR_FOREIGN || ko == PTR_FOREIGN) return MODEM_ERR_INVALID_ARG;
     DeviceGuard g(h->device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     hipStream_t s = (hipStream_t)stream;
     modem_status st;
     const float* din = in;
     float* dout = out;
-    if (n && !is_device_ptr(in)) {
+    if (ki == PTR_HOST) {
         if ((st = h->in_stage.ensure(n * sizeof(float)))) return st;
         HIP_TRY(hipMemcpyAsync(h->in_stage.p, in, n * sizeof(float), hipMemcpyHostToDevice, s));
         din = static_cast<const float*>(h->in_stage.p);
     }
-    const bool host_out = n && !is_device_ptr(out);
+    const bool host_out = ko == PTR_HOST;
     if (host_out) {
         if ((st = h->out_stage.ensure(n * sizeof(float)))) return st;
         dout = static_cast<float*>(h->out_stage.p);

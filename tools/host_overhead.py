@@ -38,6 +38,24 @@ def main():
     lib.modem_tx_sample.argtypes = [ctypes.c_void_p]
     h = d["tx"]._h
     print("ctypes trivial call us", round(per_call(lambda: lib.modem_tx_sample(h)), 2))
+    # the C entry points alone, arguments prepared once
+    L.modem_tx_process.restype = ctypes.c_int
+    prod = ctypes.c_size_t()
+    st = torch._C._cuda_getCurrentRawStream(0)
+    bp, yp, nb = d["bits"].data_ptr(), d["y"].data_ptr(), int(d["bits"].numel())
+    ny = int(d["y"].shape[0])
+    targs = (d["tx"]._h, ctypes.c_void_p(bp), ctypes.c_size_t(nb), ctypes.c_void_p(yp), ctypes.c_size_t(ny),
+             ctypes.byref(prod), ctypes.c_void_p(st))
+    print("C modem_tx_process us", round(per_call(lambda: L.modem_tx_process(*targs)), 2))
+    rargs = (d["rx"]._h, ctypes.c_void_p(yp), ctypes.c_size_t(ny), ctypes.c_void_p(d["oiq"].data_ptr()),
+             ctypes.c_void_p(d["osym"].data_ptr()), ctypes.c_size_t(int(d["oiq"].shape[0])), ctypes.byref(prod),
+             ctypes.c_void_p(st))
+    print("C modem_rx_process us", round(per_call(lambda: L.modem_rx_process(*rargs)), 2))
+    hip = ctypes.CDLL("libamdhip64.so")
+    attr = (ctypes.c_char * 256)()
+    print("hipPointerGetAttributes us", round(per_call(lambda: hip.hipPointerGetAttributes(attr, ctypes.c_void_p(yp))), 2))
+    dev = ctypes.c_int()
+    print("hipGetDevice us", round(per_call(lambda: hip.hipGetDevice(ctypes.byref(dev))), 2))
     torch.cuda.synchronize()
     pr = cProfile.Profile()
     pr.enable()
