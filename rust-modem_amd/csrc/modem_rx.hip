@@ -1157,8 +1157,8 @@ static hipError_t rxm_go_batch(const RxBatch& b, const void* tables, hipStream_t
 }
 
 // (decim, k-steps) variants: W = 32 * nks >= 15 * decim + ntaps.
-#ifdef MODEM_DEV_MIN      // experiment builds: the C2 and C3 variants only
-#define RXM_TABLE(X) X(4, 4) X(4, 6)            // C2, C3
+#ifdef MODEM_DEV_MIN      // experiment builds: the C2, C3 and C5 variants only
+#define RXM_TABLE(X) X(4, 4) X(4, 6) X(8, 20)   // C2, C3, C5
 #else
 #define RXM_TABLE(X) X(2, 2) X(2, 3) X(2, 5) X(2, 8) X(4, 3) X(4, 4) X(4, 6) X(4, 8) X(8, 5) X(8, 6) X(8, 9) X(8, 20)
 #endif

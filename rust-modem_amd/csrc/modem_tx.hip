@@ -309,7 +309,14 @@ struct TxMfma {
     static constexpr int PLN = (NE + 3 * 4 + 7) & ~7;   // halves per plane copy
     // LDS: NCOP copies x 4 planes (re_hi, re_lo, im_hi, im_lo) of PLN halves, then the split
     // LUT (4 halves per entry)
-    static constexpr int PLANES = NCOP * 4 * PLN;
+    // Halves between plane copies. ds_read2_b64 is serviced 16 lanes at a time with bank =
+    // dword mod 32 (MI355X_MICROARCH.md §LDS): with 2 copies (sps 8) the odd rows' copy must
+    // sit 28 halves past a multiple of 64, else every read of a 16-lane group is 2-way
+    // conflicted (8 extra LDS cycles per read; 13 M per C5 launch, PMC SQ_LDS_BANK_CONFLICT);
+    // with 4 copies (sps 16) a residue of 16 halves the conflicts of 0.
+    static constexpr int CRES = SB == 2 ? 28 : SB == 1 ? 16 : 0;
+    static constexpr int CST = 4 * PLN + (NCOP > 1 ? (CRES - (4 * PLN) % 64 + 64) % 64 : 0);
+    static constexpr int PLANES = NCOP * CST;
 
     // Raw bits word of symbol m, BPS bytes (fast path: aligned, no leftover bits).
     template <int BPS>
@@ -327,7 +334,7 @@ struct TxMfma {
     __device__ static void put(_Float16* pl, int e, th4 v) {
 #pragma unroll
         for (int c = 0; c < NCOP; ++c) {
-            _Float16* q = pl + c * 4 * PLN + e + c * SB;
+            _Float16* q = pl + c * CST + e + c * SB;
             q[0] = v[0]; q[PLN] = v[1]; q[2 * PLN] = v[2]; q[3 * PLN] = v[3];
         }
     }
@@ -364,7 +371,7 @@ struct TxMfma {
         const int blk = (wave * SUB + q) * 16 + i;                  // row-block in the tile
         const int cp = ((4 - ((blk * SB) & 3)) & 3) / (SB < 4 ? SB : 4);   // copy shifting the row to 8 B
         // opaque lane offset: every plane / k-step read is this base + a non-negative immediate
-        int aoff = (NCOP > 1 ? cp : 0) * 4 * PLN + blk * SB + (NCOP > 1 ? cp * SB : 0) + 8 * g;
+        int aoff = (NCOP > 1 ? cp : 0) * CST + blk * SB + (NCOP > 1 ? cp * SB : 0) + 8 * g;
         asm volatile("" : "+v"(aoff));
         const _Float16* ar = pl + aoff;
         typedef _Float16 tq4 __attribute__((ext_vector_type(4), aligned(8)));
@@ -844,8 +851,8 @@ static hipError_t txm_go_batch(TxBatch b, const void* bfrag, hipStream_t s) {
 }
 
 // (sps, k-steps) variants: W = 32 * nks >= 16/sps + K - 1 symbols (K = taps per phase).
-#ifdef MODEM_DEV_MIN      // experiment builds: the C2 and C3 variants only
-#define TXM_TABLE(X) X(4, 1) X(4, 2)            // C2, C3
+#ifdef MODEM_DEV_MIN      // experiment builds: the C2, C3 and C5 variants only
+#define TXM_TABLE(X) X(4, 1) X(4, 2) X(8, 3)    // C2, C3, C5
 #else
 #define TXM_TABLE(X) X(2, 1) X(2, 2) X(2, 3) X(2, 5) X(4, 1) X(4, 2) X(4, 3) X(4, 5) X(4, 9) \
                      X(8, 1) X(8, 2) X(8, 3) X(8, 5) X(8, 9) X(16, 1) X(16, 2) X(16, 3) X(16, 5)

@@ -44,6 +44,16 @@ __global__ void rd8c(const float4* x, float* o) {
 __global__ void cp4(const float4* x, float4* o) {
   for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N4; i += gridDim.x * blockDim.x) o[i] = x[i];
 }
+__global__ void wr4n(float4* o, float v, size_t n) {
+  for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) o[i] = make_float4(v, v, v, v);
+}
+__global__ void rd4n(const float4* x, float* o, size_t n) {
+  float4 a = make_float4(0, 0, 0, 0);
+  for (size_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float4 v = x[i]; a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  if (a.x == 12345.f) o[0] = a.y + a.z + a.w;
+}
 template <typename F> void run(const char* name, double bytes, F f) {
   f(); hipDeviceSynchronize();
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
@@ -72,6 +82,17 @@ int main() {
   run("write128+read128 (same buf)", 2 * B, [&] {
     hipLaunchKernelGGL(wr4, 2048, 256, 0, 0, y, 1.f);
     hipLaunchKernelGGL(rd4, 2048, 256, 0, 0, y, o);
+  });
+  // 512 MiB (past the 256 MiB Infinity Cache): the HBM rates a C5 launch sees
+  const size_t NB = (size_t)N4 * 4;
+  for (int g : {2048, 4096}) {
+    char n[64];
+    snprintf(n, 64, "write 512MiB float4 grid=%d", g); run(n, 4 * B, [&] { hipLaunchKernelGGL(wr4n, g, 256, 0, 0, big, 1.f, NB); });
+    snprintf(n, 64, "read 512MiB float4 grid=%d", g); run(n, 4 * B, [&] { hipLaunchKernelGGL(rd4n, g, 256, 0, 0, big, o, NB); });
+  }
+  run("write512+read512 (same buf)", 8 * B, [&] {
+    hipLaunchKernelGGL(wr4n, 4096, 256, 0, 0, big, 1.f, NB);
+    hipLaunchKernelGGL(rd4n, 4096, 256, 0, 0, big, o, NB);
   });
   return 0;
 }
