@@ -153,16 +153,15 @@ class GpuRunner:
     def kernel_times_ms(self, reps, rounds=5):
         """Mean device time of one TX launch, one RX launch and one TX+RX step, from HIP events
         on the launch stream (channel 0's launches, or the batch launches that cover every
-        channel), in the chain's context as the timed steps (and a kernel trace of this
-        command) see them: `reps` back-to-back steps between two events give the step,
-        `reps` back-to-back TX launches the TX, and the RX is the step minus the TX — the RX as
-        it runs after the TX that wrote its input (a back-to-back RX re-reading one buffer
-        runs ~2 us faster and would overstate the roofline fraction). Untimed launches are
-        queued first so that the device has a backlog (events recorded while it waits for the
-        host would time the host). Measured `rounds` times, interleaved; medians reported."""
+        channel). Each is timed directly as `reps` back-to-back launches between two events:
+        TX alone, RX alone (re-reading the sample buffer the last TX wrote, resident in HBM),
+        and the chain. Untimed launches are queued first so that the device has a backlog
+        (events recorded while it waits for the host would time the host). The three are
+        measured `rounds` times, interleaved, and the medians are reported (a single round
+        swings by a few us with the clocks)."""
         torch = self.torch
-        res = {"tx": [], "chain": []}
-        legs = (("chain", self._step_timed), ("tx", self._tx_all))
+        res = {"tx": [], "rx": [], "chain": []}
+        legs = (("chain", self._step_timed), ("tx", self._tx_all), ("rx", self._rx_all))
         for _ in range(rounds):
             for name, fn in legs:
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -175,7 +174,7 @@ class GpuRunner:
                 torch.cuda.synchronize()
                 res[name].append(ev[0].elapsed_time(ev[1]) / reps)
         med = {k: sorted(v)[rounds // 2] for k, v in res.items()}
-        return med["tx"], med["chain"] - med["tx"], med["chain"]
+        return med["tx"], med["rx"], med["chain"]
 
     def check(self):
         """Decisions of channel 0 equal the symbols sent (size-independent parity property)."""

@@ -19,6 +19,9 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
     python3 "$root/bench.py" --no-cpu-baseline > "$out/trace.log" 2>&1 || { tail -20 "$out/trace.log"; exit 3; }
 cd "$root"
+python3 tools/trace_legs.py "$out/trace/run_kernel_trace.csv" > "$out/trace_legs.json"
+grep -o '"chain_roofline": {[^}]*}' "$out/trace.log" >> "$out/trace_legs.json" || true
+cat "$out/trace_legs.json"
 echo "[4/4] pmc"
 bash tools/pmc.sh "$out/pmc" c3 || exit 4
 python3 tools/pmc_summary.py "$out/pmc" > "$out/pmc_summary.txt"
