@@ -484,6 +484,7 @@ struct RxMfma {
     static constexpr int NC = rx_mfma_table_copies(DEC);
     static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
     static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 8 * 4;   // + votes, maxima
+    static constexpr int K_TAB8 = NC * 2 * TB / 8;              // 16-B chunks of the tap tables
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
     // Waves per SIMD the registers are held to: 4 where the LDS lets 4 workgroups share a CU
     // (the matched filter then single-buffers its operands to fit 128 VGPRs), else the
@@ -854,8 +855,8 @@ struct RxMfma {
     }
 
     template <int EM>
-    __device__ static void run(const RxParams& p, _Float16* pl, const _Float16* tbl, float* red, const TileSeq sq,
-                               int64_t bid) {
+    __device__ static void run(const RxParams& p, _Float16* pl, _Float16* tbl, const _Float16* __restrict__ tables,
+                               float* red, const TileSeq sq, int64_t bid) {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
         int* votes = reinterpret_cast<int*>(red);            // [4]
@@ -867,8 +868,24 @@ struct RxMfma {
 #pragma unroll
             for (int u = 0; u < U; ++u) pre[u] = load_slot(r, voff, u);
         };
+        // the tap tables into LDS, their loads issued before the first tile's so that the two
+        // memory latencies at the kernel's start overlap (the table stores wait for the table
+        // loads only)
+        constexpr int NTB = K_TAB8 / NT + (K_TAB8 % NT ? 1 : 0);
+        h8 tv[NTB];
+#pragma unroll
+        for (int k = 0; k < NTB; ++k) {
+            const int j = tid_() + k * NT;
+            if (j < K_TAB8) tv[k] = reinterpret_cast<const h8*>(tables)[j];
+        }
         const bool f0 = cx.full(p, sq.first);
         prefetch(sq.first, f0);
+#pragma unroll
+        for (int k = 0; k < NTB; ++k) {
+            const int j = tid_() + k * NT;
+            if (j < K_TAB8) reinterpret_cast<h8*>(tbl)[j] = tv[k];
+        }
+        __syncthreads();
         // the first prediction: where the previous call ended (any exponent tile_ka can give)
         const int kin = *p.ka_in;
         int kpred = kin >= -120 && kin <= 120 && (kin & 7) == 0 ? kin : 0;
@@ -917,9 +934,6 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
     float* red = reinterpret_cast<float*>(tbl + K::NC * 2 * K::TB);
     if (bid == 0) rx_state_update<InT>(p);
-    for (int j = threadIdx.x; j < K::NC * 2 * K::TB / 8; j += K::NT)
-        reinterpret_cast<h8*>(tbl)[j] = reinterpret_cast<const h8*>(tables)[j];
-    __syncthreads();
     const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;
     // Rounds of nb tiles from the top down, tile R - (r + 1) nb + bid in round r. The TX hands
     // its tiles out grid-strided (tile i to workgroup i mod grid, both grids multiples of 8, so
@@ -931,7 +945,7 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     TileSeq sq{R - nb + bid, -nb, R / nb};
     if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }
     if (sq.count <= 0) return;
-    K::template run<EM>(p, pl, tbl, red, sq, bid);
+    K::template run<EM>(p, pl, tbl, tables, red, sq, bid);
 }
 
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>

@@ -483,7 +483,7 @@ struct TxMfma {
     // Tiles t0, t0 + ts, ... below t1. Tile t holds symbols [t*TS - lead, (t+1)*TS - lead) of the call. BPS > 0: bits aligned,
     // no leftover bits, carrier index < 2^53 (the steady state); BPS == 0: general path only.
     template <int BPS>
-    __device__ static void run(const TxParams& p, _Float16* pl, const th4* lut_s, const th8 (&bh)[NKS],
+    __device__ static void run(const TxParams& p, _Float16* pl, th4* lut_s, const th8 (&bh)[NKS],
                                const th8 (&bl)[NKS], int64_t t0, int64_t t1, int64_t ts) {
         const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int lead = p.lead;
@@ -508,9 +508,17 @@ struct TxMfma {
             }
         };
         int64_t t = t0;
+        // the first tile's bits are requested before the LUT goes to LDS, so that the two
+        // memory latencies at the kernel's start overlap
+        bool ready = t < t1 && full(t);
+        if (ready) prefetch(t);
+        const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
+        for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = lut_h[i];
+        __syncthreads();   // LUT visible
         while (t < t1) {
             if (full(t)) {
-                prefetch(t);
+                if (!ready) prefetch(t);
+                ready = false;
                 for (; t < t1 && full(t); t += ts) {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -557,15 +565,12 @@ __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __res
     th4* lut_s = reinterpret_cast<th4*>(lds_t + K::PLANES);
     const int tid = threadIdx.x, lane = tid & 63;
     if (bid == 0) tx_state_update(p);
-    const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
-    for (int i = tid; i < (1 << p.bps); i += K::NT) lut_s[i] = lut_h[i];
     th8 bh[NKS], bl[NKS];                        // this lane's B fragments (hi, lo) per k-step
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
         bh[s] = bfrag[(2 * s) * 64 + lane];
         bl[s] = bfrag[(2 * s + 1) * 64 + lane];
     }
-    __syncthreads();   // LUT visible
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
     // tiles bid, bid + nb, ...: concurrently running workgroups work on neighbouring tiles
     // (measured 1 % faster on C3 than contiguous ranges per workgroup)
