@@ -380,10 +380,13 @@ class _Dist:
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    # 500 steps of C3 are ~32 ms of device time: long enough that the timed region's fixed
-    # start/stop cost (~0.2 ms: first launch, final sync) stays under 1 % of it
-    ap.add_argument("--steps", type=int, default=500)
-    ap.add_argument("--warmup", type=int, default=50)
+    # 2000 steps of C3 are ~120 ms of device time: the timed region's fixed start/stop cost
+    # (~0.2 ms: first launch, final sync) stays well under 1 % of it. The warmup is as long:
+    # the first few ms of back-to-back launches run slower (clocks settling) — C3 measured
+    # 61.0 us/step timed after 50 warmup steps, 58.5 us after 2000 (tools/wall_probe.sh,
+    # profiles/r02_wall_probe.txt)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=2000)
     ap.add_argument("--config", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-samples", type=int, default=1 << 25)   # ~15 s of oracle work
     ap.add_argument("--no-cpu-baseline", action="store_true")

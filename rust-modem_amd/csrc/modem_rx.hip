@@ -563,6 +563,12 @@ struct RxMfma {
     __device__ static QT load_slot(__amdgpu_buffer_rsrc_t r, int voff, int u) {
         constexpr int S = sizeof(InT) * 2;
         const int o = voff + 4 * NT * u * S;
+#ifdef MODEM_RX_ABLATE_LOAD          // profiling builds only: no sample loads
+        if constexpr (std::is_same<InT, float>::value) {
+            const float v = 0.5f + 0x1p-20f * (float)(o & 1023);
+            return QT{make_float4(v, -v, v, v), make_float4(-v, v, v, -v)};
+        }
+#endif
         if constexpr (std::is_same<InT, float>::value) {
             const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
             const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, 0));
@@ -846,8 +852,16 @@ struct RxMfma {
             if (!(fi && fast_ok(votes, kpred))) return;
             f32x4 dre, dim;
             if (NWF == NW || wave < NWF) {     // uniform
+#ifdef MODEM_RX_ABLATE_FIR          // profiling builds only: no matched filter
+                dre = (f32x4){1.f, 1.f, 1.f, 1.f}; dim = dre;
+#else
                 fir(pl, tbl, dre, dim);
+#endif
+#ifdef MODEM_RX_ABLATE_STORE        // profiling builds only: no output stores
+                asm volatile("" :: "v"(dre[0] + dre[1] + dre[2] + dre[3] + dim[0] + dim[1] + dim[2] + dim[3]));
+#else
                 emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
+#endif
             }
             __syncthreads();                   // the planes are restaged next
             ++i;
