@@ -847,7 +847,12 @@ struct RxMfma {
             const bool pf = i + 1 < sq.count && cx.full(p, t + sq.step);
             const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? q_lo_of(p, t + sq.step) : 0, pf);
             const Idx ix = idx_split(p.c0 + (uint64_t)(q_lo_of(p, t) + p.n_start));
+            // the staging (VALU-bound, the limiting stage) issues ahead of the other
+            // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
+            // event, +0.8 % bench (profiles/r02_store_layout_ab.txt; priority 3: no better)
+            __builtin_amdgcn_s_setprio(1);
             stage<SC>(p, pl, votes, ix, sc, win, pre, nxt);
+            __builtin_amdgcn_s_setprio(0);
             __syncthreads();
             if (!(fi && fast_ok(votes, kpred))) return;
             f32x4 dre, dim;
