@@ -1,3 +1,6 @@
+#!/bin/bash
+# Interleaved bench A/B of two tools/build_var.sh builds (base, prio) on one box: the default
+# C3 bench line per run, without the CPU and out-of-cache legs. Usage (via gpurun): bash tools/wall_ab.sh
 for i in 1 2 3; do
  for v in base prio; do
   RUST_MODEM_AMD_LIB=$PWD/rust-modem_amd/build/var/$v/libmodem_hip.so timeout -k 10 120 python bench.py --no-cpu-baseline --no-out-of-cache > gpurun_out/wb_$v$i.json 2>gpurun_out/wb_$v$i.err || exit $?
