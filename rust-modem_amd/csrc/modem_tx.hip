@@ -533,7 +533,12 @@ struct TxMfma {
                         f32x4 dre, dim;
                         if (lv) fir<true>(pl, q, bh, bl, dre, dim);
                         else fir<false>(pl, q, bh, bl, dre, dim);
+                        // the epilogue (carrier phase, sin/cos, mix, stores) issues ahead
+                        // of the other workgroups' staging and filter: +0.6 % C3 bench in
+                        // three interleaved pairs (profiles/r02_store_layout_ab.txt)
+                        __builtin_amdgcn_s_setprio(1);
                         emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
+                        __builtin_amdgcn_s_setprio(0);
                     }
                     __syncthreads();                     // the window is restaged next trip
                 }
