@@ -150,49 +150,91 @@ class GpuRunner:
         else:
             self.rx(0)
 
-    def kernel_times_ms(self, reps, rounds=5):
+    def kernel_times_ms(self, budget_ms=10.0, min_reps=200, rounds=5):
         """Mean device time of one TX launch, one RX launch and one TX+RX step, from HIP events
         on the launch stream (channel 0's launches, or the batch launches that cover every
-        channel). Each is timed directly as `reps` back-to-back launches between two events:
-        TX alone, RX alone (re-reading the sample buffer the last TX wrote, resident in HBM),
-        and the chain. Untimed launches are queued first so that the device has a backlog
-        (events recorded while it waits for the host would time the host). The three are
-        measured `rounds` times, interleaved, and the medians are reported (a single round
-        swings by a few us with the clocks)."""
+        channel). Each leg is timed directly as back-to-back launches between two events: TX
+        alone, RX alone (re-reading the sample buffer the last TX wrote, resident in HBM), and
+        the chain. The amount of work is a device-time budget, independent of --steps (the
+        driver's 20 steps are ~1 ms of C3, while the clock settles over the first few ms of
+        back-to-back launches: profiles/r02_wall_probe.txt): per leg and round an untimed
+        backlog of >= budget_ms (so that events are never recorded while the device waits for
+        the host), then max(min_reps, budget_ms of launches) timed. Rounds are interleaved and
+        the medians reported (a single round swings by a few us with the clocks)."""
         torch = self.torch
-        res = {"tx": [], "rx": [], "chain": []}
         legs = (("chain", self._step_timed), ("tx", self._tx_all), ("rx", self._rx_all))
+        est = {}
+        for name, fn in legs:                  # per-launch estimate, for the budget
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            for _ in range(4):
+                fn()
+            ev[0].record(self.stream)
+            for _ in range(8):
+                fn()
+            ev[1].record(self.stream)
+            torch.cuda.synchronize()
+            est[name] = max(ev[0].elapsed_time(ev[1]) / 8, 1e-4)
+        res = {"tx": [], "rx": [], "chain": []}
+        reps = {}
         for _ in range(rounds):
             for name, fn in legs:
+                n_back = max(8, int(budget_ms / est[name]) + 1)
+                n = reps[name] = max(min_reps, int(budget_ms / est[name]) + 1)
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                for _ in range(8):
+                for _ in range(n_back):
                     fn()
                 ev[0].record(self.stream)
-                for _ in range(reps):
+                for _ in range(n):
                     fn()
                 ev[1].record(self.stream)
                 torch.cuda.synchronize()
-                res[name].append(ev[0].elapsed_time(ev[1]) / reps)
+                res[name].append(ev[0].elapsed_time(ev[1]) / n)
         med = {k: sorted(v)[rounds // 2] for k, v in res.items()}
+        self.leg_reps = reps
         return med["tx"], med["rx"], med["chain"]
 
-    def check(self):
-        """Decisions of channel 0 equal the symbols sent (size-independent parity property)."""
+    def sent_symbols(self, c):
         torch = self.torch
-        d = self.ch[0]
-        b = d["bits"].view(-1, self.bps).to(torch.int64)
+        b = self.ch[c]["bits"].view(-1, self.bps).to(torch.int64)
         wts = torch.tensor([1 << (self.bps - 1 - k) for k in range(self.bps)], device=b.device)
-        sent = (b * wts).sum(1).to(torch.uint8)
-        # the stream continues across steps: re-run one clean pass on fresh handles is costly,
-        # so compare the decisions the last RX call produced against the symbols they refer to
-        nout = d["nout"]
-        got = d["osym"][:nout]
-        # steady state: RX call j decides symbols k in [j*nsym - (L-1)/sps, ...) of the stream;
-        # symbol k of call j == symbol (k mod nsym) of the (repeated) batch
-        lag = (self.L - 1 + self.sps - 1) // self.sps
-        nsym = self.nsamp // self.sps
-        idx = (torch.arange(nout, device=b.device) - lag) % nsym
-        return bool(torch.equal(got, sent[idx]))
+        return (b * wts).sum(1).to(torch.uint8)
+
+    def check(self):
+        """The decisions of every channel equal the symbols that channel sent (size-independent
+        parity property)."""
+        torch = self.torch
+        for c, d in enumerate(self.ch):
+            sent = self.sent_symbols(c)
+            # the stream continues across steps; the last RX call of a channel decides symbols
+            # k in [j*nsym - (L-1)/sps, ...) of its stream, and symbol k of call j is symbol
+            # (k mod nsym) of the (repeated) batch
+            nout = d["nout"]
+            got = d["osym"][:nout]
+            lag = (self.L - 1 + self.sps - 1) // self.sps
+            nsym = self.nsamp // self.sps
+            idx = (torch.arange(nout, device=got.device) - lag) % nsym
+            if not torch.equal(got, sent[idx]):
+                return False
+        return True
+
+    def gather_ms(self, reps=5):
+        """SURVEY.md §8e's final host gather: the D2H copy of this GPU's u8 decisions (every
+        channel) into pinned host memory, on the launch stream, timed by HIP events (median of
+        `reps`). Returns (ms, bytes)."""
+        torch = self.torch
+        host = [torch.empty(d["nout"], dtype=torch.uint8, pin_memory=True) for d in self.ch]
+        nbytes = sum(d["nout"] for d in self.ch)
+        ts = []
+        for _ in range(reps):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+            ev[0].record(self.stream)
+            for h, d in zip(host, self.ch):
+                h.copy_(d["osym"][:d["nout"]], non_blocking=True)
+            ev[1].record(self.stream)
+            torch.cuda.synchronize()
+            ts.append(ev[0].elapsed_time(ev[1]))
+        self.gathered = host
+        return sorted(ts)[reps // 2], nbytes
 
 
 def _cpu_threads():
@@ -290,7 +332,11 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
     total = nsamp * nch * args.steps * world
     value = total / dt / 1e6
     ok = r.check()
-    t_tx, t_rx, t_chain = r.kernel_times_ms(max(20, min(args.steps, 100)))
+    g_ms, g_bytes = r.gather_ms()
+    if dist is not None:
+        ok = dist.max_over_ranks(0.0 if ok else 1.0) == 0.0
+        g_ms = dist.max_over_ranks(g_ms)
+    t_tx, t_rx, t_chain = r.kernel_times_ms()
     b_tx, b_rx, nout = algorithmic_bytes(bps, L, sps, nsamp, dtype)
     per_launch = nch if getattr(r, "batch", False) else 1      # channels one timed launch covers
     b_tx, b_rx, nsamp_launch = b_tx * per_launch, b_rx * per_launch, nsamp * per_launch
@@ -324,9 +370,17 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
         "chain_roofline": {"tx_ms": round(t_tx, 5), "rx_ms": round(t_rx, 5), "chain_ms": round(t_chain, 5),
                            "tx_bytes": b_tx, "rx_bytes": b_rx,
                            "bytes_per_sample": round((b_tx + b_rx) / nsamp_launch, 4),
+                           "rx_in_chain_ms": round(t_chain - t_tx, 5),
+                           "rx_in_chain_frac": round(b_rx / ((t_chain - t_tx) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "reps_per_leg": getattr(r, "leg_reps", None),
                            "achieved": round(chain_gbs, 1), "frac": round(chain_gbs / HBM_PEAK_GBS, 4),
                            "device_msamples_per_s": round(nsamp_launch / (t_chain * 1e-3) / 1e6, 1)},
         "decisions_match_sent": ok,
+        # the host gather of the decisions, timed separately from `value`
+        "gather": {"ms": round(g_ms, 5), "bytes_per_gpu": g_bytes,
+                   "gb_per_s": round(g_bytes / (g_ms * 1e-3) / 1e9, 2) if g_ms > 0 else None,
+                   "what": "D2H of every rank's u8 decisions (all channels) into pinned host memory, "
+                           "HIP events on the launch stream, max over ranks; not in the timed region"},
     }
     if args.amplitude != 1.0:
         out["config"]["amplitude"] = args.amplitude
@@ -360,6 +414,9 @@ def out_of_cache_roofline(runner_factory, config="c5"):
 
 
 class _Dist:
+    """Timing barrier and max-over-ranks reduction. `device` None: gloo on the host (ranks that
+    share a GPU, or CPU tests); else nccl (= RCCL) on this rank's GPU."""
+
     def __init__(self, td, device):
         self.td, self.device = td, device
 
@@ -377,8 +434,10 @@ class _Dist:
         return float(t.item())
 
 
-def main(argv=None):
+def _parser():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    # GPUs of this node: under a launcher (torch.distributed.run: WORLD_SIZE set) it must equal
+    # WORLD_SIZE; without one, N > 1 starts N rank processes itself (one per GPU)
     ap.add_argument("--gpus", type=int, default=1)
     # 2000 steps of C3 are ~120 ms of device time: the timed region's fixed start/stop cost
     # (~0.2 ms: first launch, final sync) stays well under 1 % of it. The warmup is as long:
@@ -400,26 +459,85 @@ def main(argv=None):
     ap.add_argument("--amplitude", type=float, default=1.0)
     # skip the C5 f32 out-of-Infinity-Cache roofline measured after the C3 line
     ap.add_argument("--no-out-of-cache", action="store_true")
-    args = ap.parse_args(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return ap
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn(args, argv):
+    """--gpus N without a launcher: N fresh rank processes (`python bench.py` with RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* set), started before this process touches the GPU (it
+    never does). Rank 0's JSON line is printed and returned; the exit status is the worst of
+    the ranks'."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    procs = []
+    for r in range(args.gpus):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out0 = procs[0].communicate()[0]
+    rcs = [p.wait() for p in procs]
+    line = None
+    for ln in (out0 or "").splitlines():
+        if ln.startswith("{"):
+            line = ln
+    if line is not None:
+        print(line, flush=True)
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        raise SystemExit(bad[0])
+    if line is None:
+        raise SystemExit(1)
+    return json.loads(line)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = _parser().parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    wenv = os.environ.get("WORLD_SIZE")
+    if wenv is None and args.gpus > 1:
+        return _spawn(args, argv)
+    world = int(wenv or "1")
+    if wenv is not None and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world} of the launcher",
+              file=sys.stderr)
+        raise SystemExit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local
     if world > 1:
         import torch
         import torch.distributed as td
-        torch.cuda.set_device(local)
-        td.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        dist = _Dist(td, local)
+        ndev = torch.cuda.device_count()
+        if ndev < 1:
+            raise SystemExit("bench.py: no GPU")
+        device = local % ndev
+        torch.cuda.set_device(device)
+        if world <= ndev:     # one GPU per rank: RCCL for the barrier and the max over ranks
+            td.init_process_group("nccl", device_id=torch.device(f"cuda:{device}"))
+            dist = _Dist(td, device)
+        else:                 # ranks share a GPU (a one-GPU box): RCCL cannot, gloo on the host
+            td.init_process_group("gloo")
+            dist = _Dist(td, None)
     nch = WORKLOADS[args.config][5]
     nst = args.streams if args.streams > 0 else min(nch, 4)
     batch = nch > 1 and not args.no_batch
-    out = run(args, lambda wl, r: GpuRunner(wl, r, local, 1 if batch else nst, batch, args.amplitude),
+    out = run(args, lambda wl, r: GpuRunner(wl, r, device, 1 if batch else nst, batch, args.amplitude),
               dist, rank, world)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.td.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":

@@ -233,7 +233,7 @@ class Carrier:
         out = torch.empty(int(n), dtype=torch.float32, device=f"cuda:{device}")
         _check(load_library().modem_carrier_phases(self.sample_freq, int(s0), int(n),
                                                    out.data_ptr() if n else None, device,
-                                                   _stream_handle(stream)), "Carrier.phases")
+                                                   _stream_handle(stream, device)), "Carrier.phases")
         return out
 
 
@@ -495,13 +495,19 @@ def _torch_cuda():
     return _TORCH
 
 
-def _stream_handle(stream) -> Optional[int]:
+def _stream_handle(stream, device: Optional[int] = None) -> Optional[int]:
+    """The raw HIP stream a call is queued on: `stream` (a torch Stream or a raw handle), else
+    torch's current stream of `device` (the handle's GPU; None: the current device), so that
+    a handle on another GPU never launches on this device's stream."""
     if stream is not None:
+        sdev = getattr(stream, "device_index", None)
+        if device is not None and sdev is not None and int(sdev) != int(device):
+            raise ValueError(f"stream of cuda:{sdev} given to a handle on cuda:{device}")
         return int(getattr(stream, "cuda_stream", stream))
     t = _torch_cuda()
     if t:
         # the current stream's raw handle (current_stream() builds a Stream object: ~3 us)
-        return t._C._cuda_getCurrentRawStream(t._C._cuda_getDevice())
+        return t._C._cuda_getCurrentRawStream(t._C._cuda_getDevice() if device is None else int(device))
     return None
 
 
@@ -592,7 +598,7 @@ class DigitalModulator:
         cap = int(out.shape[0])
         prod = ctypes.c_size_t()
         _check(load_library().modem_tx_process(self._h, _ptr(bits), n, _ptr(out), cap,
-                                               ctypes.byref(prod), _stream_handle(stream)),
+                                               ctypes.byref(prod), _stream_handle(stream, self.device)),
                "DigitalModulator.process")
         self._ncarry = (self._ncarry + n) % self.bps
         self.carrier.sample += prod.value        # = modem_tx_sample(h): one sample per output
@@ -615,7 +621,7 @@ class DigitalModulator:
         prod = (sz * n)()
         _check(load_library().modem_tx_process_batch(
             hs, n, (vp * n)(*[_ptr(b) for b in bits]), (sz * n)(*nb), (vp * n)(*[_ptr(o) for o in outs]),
-            (sz * n)(*[int(o.shape[0]) for o in outs]), prod, _stream_handle(stream)),
+            (sz * n)(*[int(o.shape[0]) for o in outs]), prod, _stream_handle(stream, mods[0].device)),
             "DigitalModulator.process_batch")
         for m, k in zip(mods, nb):
             m._ncarry = (m._ncarry + k) % m.bps
@@ -630,7 +636,7 @@ class DigitalModulator:
         out = self._alloc(ref, ns)
         prod = ctypes.c_size_t()
         _check(load_library().modem_tx_flush(self._h, _ptr(out), int(out.shape[0]), ctypes.byref(prod),
-                                             _stream_handle(stream)), "DigitalModulator.flush")
+                                             _stream_handle(stream, self.device)), "DigitalModulator.flush")
         self.carrier.sample = int(load_library().modem_tx_sample(self._h))
         return out[: prod.value]
 
@@ -664,7 +670,7 @@ class TxBatchPlan:
     def run(self, stream=None):
         """Returns the samples produced per channel (written to outs[c][:produced[c]])."""
         _check(self._fn(self._hs, self.n, self._bits, self._nbits, self._outs, self._caps, self._prod,
-                        _stream_handle(stream)), "TxBatchPlan.run")
+                        _stream_handle(stream, self.mods[0].device)), "TxBatchPlan.run")
         L = load_library()
         for m, k in zip(self.mods, self._nb):
             m._ncarry = (m._ncarry + k) % m.bps
@@ -673,6 +679,27 @@ class TxBatchPlan:
 
 
 # ------------------------------------------------------------------- RX (B6+B5) ----
+_IN_DTYPE_NAME = {DTYPE_F32: "float32", DTYPE_F16: "float16", DTYPE_I16: "int16"}
+
+
+def _dtype_name(x) -> str:
+    return str(getattr(x, "dtype", "")).replace("torch.", "")
+
+
+def _check_rx_input(x, in_dtype: int, what: str) -> int:
+    """The input must be what the handle was created for — (n, 2) float32 / float16 (i, q) or
+    (n,) int16 real samples — else the C side would read n samples of the wrong width.
+    Returns n."""
+    want = _IN_DTYPE_NAME.get(in_dtype)
+    got = _dtype_name(x)
+    shape = tuple(int(d) for d in x.shape)
+    ok_shape = len(shape) == 1 if in_dtype == DTYPE_I16 else (len(shape) == 2 and shape[1] == 2)
+    if got != want or not ok_shape:
+        form = "(n,) int16" if in_dtype == DTYPE_I16 else f"(n, 2) {want}"
+        raise ValueError(f"{what}: input must be {form} (the handle's in_dtype), got {shape} {got}")
+    return shape[0]
+
+
 class DemodulatorRx:
     """Demodulator (demodulator.rs:7-56) + matched filter + decimation + slicer.
 
@@ -687,6 +714,7 @@ class DemodulatorRx:
                  phase_offset: float = 0.0):
         L = load_library()
         self.carrier, self.decim, self.out_dtype, self.in_dtype = carrier, int(decim), out_dtype, in_dtype
+        self.device = device
         self.taps = np.ascontiguousarray(taps, dtype=np.float32)
         self.decim_offset = int(decim_offset)
         d = _RxDesc()
@@ -715,7 +743,7 @@ class DemodulatorRx:
 
     def process(self, iq, want_iq: bool = True, want_sym: bool = True, stream=None,
                 out_iq=None, out_sym=None):
-        n = int(iq.shape[0])
+        n = _check_rx_input(iq, self.in_dtype, "Demodulator.process")
         nout = self.noutputs(n)
         npd = np.float16 if self.out_dtype == DTYPE_F16 else np.float32
         oiq = out_iq if out_iq is not None else (_empty_like_input(iq, (nout, 2), npd) if want_iq else None)
@@ -724,7 +752,7 @@ class DemodulatorRx:
         cap = min(int(oiq.shape[0]) if oiq is not None else nout, int(osym.shape[0]) if osym is not None else nout)
         prod = ctypes.c_size_t()
         _check(load_library().modem_rx_process(self._h, _ptr(iq), n, _ptr(oiq), _ptr(osym), cap,
-                                               ctypes.byref(prod), _stream_handle(stream)),
+                                               ctypes.byref(prod), _stream_handle(stream, self.device)),
                "Demodulator.process")
         self._consumed += n
         self.carrier.sample += n                 # = modem_rx_sample(h): one per input sample
@@ -741,7 +769,7 @@ class DemodulatorRx:
         if len(rxs) != len(iqs) or len(set(map(id, rxs))) != len(rxs):
             raise ValueError("one input buffer per distinct demodulator")
         n = len(rxs)
-        ns = [int(x.shape[0]) for x in iqs]
+        ns = [_check_rx_input(x, r.in_dtype, "Demodulator.process_batch") for r, x in zip(rxs, iqs)]
         nouts = [r.noutputs(k) for r, k in zip(rxs, ns)]
         if out_iq is None:
             out_iq = [_empty_like_input(x, (k, 2), np.float16 if r.out_dtype == DTYPE_F16 else np.float32)
@@ -756,7 +784,7 @@ class DemodulatorRx:
         _check(load_library().modem_rx_process_batch(
             (vp * n)(*[r._h.value for r in rxs]), n, (vp * n)(*[_ptr(x) for x in iqs]), (sz * n)(*ns),
             (vp * n)(*[_ptr(a) or None for a in out_iq]), (vp * n)(*[_ptr(b) or None for b in out_sym]),
-            (sz * n)(*caps), prod, _stream_handle(stream)), "Demodulator.process_batch")
+            (sz * n)(*caps), prod, _stream_handle(stream, rxs[0].device)), "Demodulator.process_batch")
         res = []
         for i, (r, k) in enumerate(zip(rxs, ns)):
             r._consumed += k
@@ -774,7 +802,7 @@ class DemodulatorRx:
         osym = _empty_like_input(ref, (nout,), np.uint8) if self._slicer is not None else None
         prod = ctypes.c_size_t()
         _check(load_library().modem_rx_flush(self._h, _ptr(oiq), _ptr(osym), nout, ctypes.byref(prod),
-                                             _stream_handle(stream)), "Demodulator.flush")
+                                             _stream_handle(stream, self.device)), "Demodulator.flush")
         self._consumed += n
         self.carrier.sample = int(load_library().modem_rx_sample(self._h))
         return oiq[: prod.value], (None if osym is None else osym[: prod.value])
@@ -821,7 +849,10 @@ class Demodulator:
     def process(self, sig, stream=None):
         """(n, 2) float32 (i, q), one per input sample (Iterator::next, demodulator.rs:44-56)."""
         if self._rx is None:
-            i16 = str(getattr(sig, "dtype", "")).endswith("int16")
+            i16 = _dtype_name(sig) == "int16"
+            if i16 and not self.exact:
+                raise ValueError("Demodulator.process: int16 input needs exact=True "
+                                 "(MIX_REFERENCE_REAL_EXACT reads i16 samples; the fast real mix does not)")
             self._rx = DemodulatorRx(self.carrier, self.lowpass, decim=1, decim_offset=0,
                                      mix=MIX_REFERENCE_REAL_EXACT if self.exact else MIX_REFERENCE_REAL,
                                      in_dtype=DTYPE_I16 if i16 else DTYPE_F32, device=self.device,
@@ -834,6 +865,7 @@ class FIRFilter:
     """FIRFilter (fir.rs:3-35): causal FIR, zero initial history, one output per input."""
 
     def __init__(self, coefs, device: int = 0):
+        self.device = device
         self.coefs = np.ascontiguousarray(coefs, dtype=np.float32)
         if len(self.coefs) == 0:
             raise ModemPanic(ERR_INVALID_ARG, "FIRFilter: attempt to calculate the remainder with a divisor of zero")
@@ -845,7 +877,7 @@ class FIRFilter:
     def process(self, x, stream=None):
         n = int(x.shape[0])
         y = _empty_like_input(x, (n,), np.float32)
-        _check(load_library().modem_fir_process(self._h, _ptr(x), _ptr(y), n, _stream_handle(stream)),
+        _check(load_library().modem_fir_process(self._h, _ptr(x), _ptr(y), n, _stream_handle(stream, self.device)),
                "FIRFilter.process")
         return y
 
@@ -869,7 +901,7 @@ class RxBatchPlan:
         if len(self.iqs) != n or len(out_iq) != n or len(out_sym) != n or len(set(map(id, self.rxs))) != n:
             raise ValueError("one input and one output set per distinct demodulator")
         vp, sz = ctypes.c_void_p, ctypes.c_size_t
-        self._ns = [int(x.shape[0]) for x in self.iqs]
+        self._ns = [_check_rx_input(x, r.in_dtype, "RxBatchPlan") for r, x in zip(self.rxs, self.iqs)]
         caps = [min(int(a.shape[0]) if a is not None else 1 << 62, int(b.shape[0]) if b is not None else 1 << 62)
                 for a, b in zip(out_iq, out_sym)]
         self._hs = (vp * n)(*[r._h.value for r in self.rxs])
@@ -884,7 +916,7 @@ class RxBatchPlan:
     def run(self, stream=None):
         """Returns the kept instants produced per channel."""
         _check(self._fn(self._hs, self.n, self._ins, self._nsa, self._oiq, self._osym, self._caps, self._prod,
-                        _stream_handle(stream)), "RxBatchPlan.run")
+                        _stream_handle(stream, self.rxs[0].device)), "RxBatchPlan.run")
         L = load_library()
         for r, k in zip(self.rxs, self._ns):
             r._consumed += k
@@ -897,5 +929,5 @@ def prng_bits(seed: int, nbits: int, device: int = 0, stream=None):
     import torch
     out = torch.empty(int(nbits), dtype=torch.uint8, device=f"cuda:{device}")
     _check(load_library().modem_prng_bits(int(seed), out.data_ptr() if nbits else None, int(nbits), device,
-                                          _stream_handle(stream)), "prng_bits")
+                                          _stream_handle(stream, device)), "prng_bits")
     return out

@@ -10,6 +10,16 @@
 // Compiled by hipcc (device code: the bit-exact demodulator, mix MODEM_MIX_REFERENCE_REAL_EXACT)
 // and by gcc (tools/libm_check.c compares it with the host's sinf / cosf for every float).
 // Every operation is explicit (no contraction left to the compiler).
+//
+// Attribution: the algorithm and its constants (the polynomial coefficients of sincos_t and the
+// 4/pi bit table __inv_pio4) are those of ARM's optimized-routines single-precision sinf/cosf
+// (Szabolcs Nagy, Arm Ltd., 2018), as contributed to and shipped in the GNU C Library
+// (sysdeps/ieee754/flt-32/{s_sinf.c, s_cosf.c, sincosf.h, sincosf_poly.h}; glibc 2.35). In
+// glibc those files are distributed under the GNU Lesser General Public License v2.1 or later;
+// optimized-routines itself is available under the MIT OR Apache-2.0 WITH LLVM-exception
+// licenses. This file restates that published algorithm for the device; no glibc source text
+// is copied. The numeric constants are facts of the reference platform's libm that bit-exact
+// parity with Rust's f32::sin / f32::cos on it requires.
 #pragma once
 #include <stdint.h>
 #include <string.h>

@@ -50,12 +50,21 @@ class CpuRunner:
     def sync(self):
         pass
 
-    def kernel_times_ms(self, reps, rounds=5):
+    def kernel_times_ms(self, *a, **k):
         return 0.01, 0.02, 0.03
 
+    def gather_ms(self):
+        # the host gather of every channel's decisions (here already host arrays)
+        t0 = time.perf_counter()
+        self.gathered = [np.array(x, copy=True) for x in self.out]
+        return (time.perf_counter() - t0) * 1e3, sum(len(x) for x in self.out)
+
     def check(self):
-        sent = self.bits[0].reshape(-1, self.bps).astype(np.int64) @ (1 << np.arange(self.bps)[::-1])
-        return bool(np.array_equal(self.out[0], sent[: len(self.out[0])].astype(np.uint8)))
+        for b, got in zip(self.bits, self.out):
+            sent = b.reshape(-1, self.bps).astype(np.int64) @ (1 << np.arange(self.bps)[::-1])
+            if not np.array_equal(got, sent[: len(got)].astype(np.uint8)):
+                return False
+        return True
 
 
 def _worker(rank, world, port, outdir):
@@ -97,6 +106,55 @@ def test_two_ranks_gloo(tmp_path):
     assert abs(outs[0]["value"] - total / (outs[0]["ms_per_step"] * 3 / 1e3) / 1e6) <= 0.02 * outs[0]["value"]
     # ranks own disjoint channels
     assert not set(outs[0]["_seeds"]) & set(outs[1]["_seeds"])
+    # the host gather of the decisions, timed apart from `value`, max over ranks
+    for out in outs:
+        g = out["gather"]
+        assert g["bytes_per_gpu"] == 2 * (((1 << 12) - 128) // 4) and g["ms"] >= 0   # L - 1 = 128 samples of lag
+    assert outs[0]["gather"]["ms"] == outs[1]["gather"]["ms"]
+
+
+def test_gpus_flag_must_match_launcher(monkeypatch):
+    """Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE: bench.py exits 2 before
+    touching a GPU instead of timing a different node size than the line reports."""
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "1"])
+    assert e.value.code == 2
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "4"])
+    assert e.value.code == 2
+
+
+def test_gpus_flag_spawns_ranks(monkeypatch):
+    """Without a launcher, --gpus N starts N rank processes (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set, one port for all) and returns rank 0's line; the parent itself never imports
+    torch.cuda. The child processes are stubbed here (no GPU on the CPU runner)."""
+    import subprocess
+    import bench
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    started = []
+
+    class FakePopen:
+        def __init__(self, cmd, env, stdout, text):
+            started.append((cmd, {k: env[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}))
+            self.rank = int(env["RANK"])
+
+        def communicate(self):
+            line = json.dumps({"n_gpus": 4, "value": 1.0}) if self.rank == 0 else ""
+            return ("log line\n" + line + "\n", None)
+
+        def wait(self):
+            return 0
+
+    monkeypatch.setattr(subprocess, "Popen", FakePopen)
+    out = bench.main(["--gpus", "4", "--config", "c4", "--steps", "3"])
+    assert out == {"n_gpus": 4, "value": 1.0}
+    assert [e["RANK"] for _, e in started] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1" for _, e in started)
+    assert len({e["MASTER_PORT"] for _, e in started}) == 1
+    assert all(cmd[-6:] == ["--gpus", "4", "--config", "c4", "--steps", "3"] for cmd, _ in started)
 
 
 def test_cpu_baseline_multicore_leg():

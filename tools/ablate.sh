@@ -1,14 +1,19 @@
 #!/bin/bash
 # Build ablation variants of the backend (profiling only) into rust-modem_amd/build/ablate/<v>/.
-# Each variant drops one stage of the kernels so its cost shows up as a time difference:
-# FIR (no matrix products), TRIG (no sin/cos), MIX (no carrier mix at all), STORE (no
-# output stores; TX only). Usage: tools/ablate.sh [variants...]
+# Each variant drops one stage of the kernels so its cost shows up as a time difference.
+# TX (-DMODEM_ABLATE_<v>): FIR (no matrix products), TRIG (no sin/cos), MIX (no carrier mix),
+# STORE (no output stores). RX (-DMODEM_RX_ABLATE_<v>): RX_LOAD (no sample loads), RX_FIR
+# (no matched filter), RX_STORE (no output stores). Usage: tools/ablate.sh [variants...]
 set -e
 cd "$(dirname "$0")/../rust-modem_amd"
-vars=${@:-base FIR TRIG MIX STORE}
+vars=${@:-base FIR TRIG MIX STORE RX_LOAD RX_FIR RX_STORE}
 for v in $vars; do
   d=build/ablate/$v; mkdir -p $d
-  extra=""; [ "$v" != base ] && extra="-DMODEM_ABLATE_$v"
+  case $v in
+    base) extra="" ;;
+    RX_*) extra="-DMODEM_RX_ABLATE_${v#RX_}" ;;
+    *) extra="-DMODEM_ABLATE_$v" ;;
+  esac
   for f in tx rx misc; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 $extra -c csrc/modem_$f.hip -o $d/$f.o &
   done

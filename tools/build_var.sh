@@ -1,6 +1,6 @@
 #!/bin/bash
 # Experiment build of the backend restricted to the C3 kernels (-DMODEM_DEV_MIN), plus any
-# extra flags, into rust-modem_amd/build/var/<name>/libmodem_hip.so (A/B with tools/ab_run.sh).
+# extra flags, into rust-modem_amd/build/var/<name>/libmodem_hip.so (A/B with tools/ab.sh).
 # Usage: tools/build_var.sh <name> [hipcc flags...]
 set -e
 name=$1; shift

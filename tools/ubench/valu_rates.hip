@@ -42,6 +42,42 @@ __global__ void k_lds(float* o, int stride) {
   }
   o[blockIdx.x * blockDim.x + threadIdx.x] = acc.x + acc.y;
 }
+// 16 independent fma + 4 independent v_sin per iteration: does the transcendental unit
+// overlap the FMA pipe (time ~ max) or share it (time ~ sum)?
+__global__ void k_fma_sin(float* o, float s) {
+  float a[16], b[4]; for (int i = 0; i < 16; ++i) a[i] = threadIdx.x + i;
+  for (int i = 0; i < 4; ++i) b[i] = threadIdx.x * 1e-3f + i;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = __builtin_fmaf(a[i], s, 0.5f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = __builtin_amdgcn_sinf(b[i]);
+  }
+  float t = 0; for (int i = 0; i < 16; ++i) t += a[i]; for (int i = 0; i < 4; ++i) t += b[i];
+  o[blockIdx.x * blockDim.x + threadIdx.x] = t;
+}
+// dependent chains (latency): 2 independent chains per lane
+__global__ void k_fma_dep(float* o, float s) {
+  float a = threadIdx.x, b = threadIdx.x + 1;
+  for (int it = 0; it < ITERS * 8; ++it) { a = __builtin_fmaf(a, s, 0.5f); b = __builtin_fmaf(b, s, 0.25f); }
+  o[blockIdx.x * blockDim.x + threadIdx.x] = a + b;
+}
+__global__ void k_pkfma_dep(float* o, float s) {
+  f2 a = {(float)threadIdx.x, 1.f}, b = {2.f, (float)threadIdx.x};
+  for (int it = 0; it < ITERS * 8; ++it) {
+    a = __builtin_elementwise_fma(a, (f2){s, s}, (f2){0.5f, 0.25f});
+    b = __builtin_elementwise_fma(b, (f2){s, s}, (f2){0.5f, 0.25f});
+  }
+  o[blockIdx.x * blockDim.x + threadIdx.x] = a.x + a.y + b.x + b.y;
+}
+__global__ void k_floor(float* o, float s) {
+  float a[16]; for (int i = 0; i < 16; ++i) a[i] = threadIdx.x * 0.37f + i;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = __builtin_floorf(a[i] * s);
+  }
+  float t = 0; for (int i = 0; i < 16; ++i) t += a[i]; o[blockIdx.x * blockDim.x + threadIdx.x] = t;
+}
 template <typename F> double run(F f, const char* name, double ops_per_lane, int blocks, int threads) {
   float* o; hipMalloc(&o, (size_t)blocks * threads * 4);
   f(o); hipDeviceSynchronize();
@@ -56,12 +92,19 @@ template <typename F> double run(F f, const char* name, double ops_per_lane, int
   hipFree(o); return ms;
 }
 int main() {
-  const int B = 256 * 8, T = 256;   // 8 waves / SIMD
+  for (int occ = 4; occ <= 8; occ += 4) {
+  const int B = 256 * occ, T = 256;   // occ waves / SIMD
+  printf("== %d waves per SIMD\n", occ);
+  run([&](float* o) { hipLaunchKernelGGL(k_fma_sin, B, T, 0, 0, o, 0.999f); }, "16 fma + 4 sin (per 16 fma)", ITERS * 16.0, B, T);
+  run([&](float* o) { hipLaunchKernelGGL(k_fma_dep, B, T, 0, 0, o, 0.999f); }, "v_fma_f32 2 dep chains", ITERS * 16.0, B, T);
+  run([&](float* o) { hipLaunchKernelGGL(k_pkfma_dep, B, T, 0, 0, o, 0.999f); }, "v_pk_fma_f32 2 dep chains", ITERS * 16.0, B, T);
+  run([&](float* o) { hipLaunchKernelGGL(k_floor, B, T, 0, 0, o, 0.999f); }, "v_mul+v_floor (per pair)", ITERS * 16.0, B, T);
   run([&](float* o) { hipLaunchKernelGGL(k_fma, B, T, 0, 0, o, 0.999f); }, "v_fma_f32", ITERS * 16.0, B, T);
   run([&](float* o) { hipLaunchKernelGGL(k_pkfma, B, T, 0, 0, o, 0.999f); }, "v_pk_fma_f32", ITERS * 16.0, B, T);
   run([&](float* o) { hipLaunchKernelGGL(k_sin, B, T, 0, 0, o, 0.999f); }, "v_sin_f32", ITERS * 16.0, B, T);
   run([&](float* o) { hipLaunchKernelGGL(k_lds, B / 2, T, 0, 0, o, 1); }, "ds_read_b64 stride8B(+add)", ITERS * 16.0, B / 2, T);
   run([&](float* o) { hipLaunchKernelGGL(k_lds, B / 2, T, 0, 0, o, 2); }, "ds_read_b64 stride16B(+add)", ITERS * 16.0, B / 2, T);
   run([&](float* o) { hipLaunchKernelGGL(k_lds, B / 2, T, 0, 0, o, 5); }, "ds_read_b64 stride40B(+add)", ITERS * 16.0, B / 2, T);
+  }
   return 0;
 }
