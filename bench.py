@@ -103,6 +103,12 @@ class GpuRunner:
             self._txp = m.TxBatchPlan([d["tx"] for d in ch], [d["bits"] for d in ch], [d["y"] for d in ch])
             self._rxp = m.RxBatchPlan([d["rx"] for d in ch], [d["y"] for d in ch], [d["oiq"] for d in ch],
                                       [d["osym"] for d in ch])
+        # one prepared C call per channel and step (modem_chain_run = modem_tx_process +
+        # modem_rx_process on the fixed device buffers): the TX and RX kernels of the step with
+        # the buffers checked once, so that the host stays ahead of small steps (C2)
+        chain = hasattr(m.load_library(), "modem_chain_run")   # (experiment builds of older sources: no)
+        self._plans = None if batch or not chain else [
+            m.ChainPlan(d["tx"], d["rx"], d["bits"], d["y"], d["oiq"], d["osym"]) for d in self.ch]
         torch.cuda.synchronize()
 
     def tx(self, c, stream=None):
@@ -117,6 +123,10 @@ class GpuRunner:
         if self.batch:
             self._txp.run()
             self._rxp.run()
+            return
+        if len(self.streams) == 1 and self._plans:
+            for pl in self._plans:
+                pl.run()
             return
         if len(self.streams) > 1:
             for st in self.streams[1:]:
@@ -140,6 +150,8 @@ class GpuRunner:
     def _step_timed(self):
         if self.batch:
             self.step()
+        elif self._plans:
+            self._plans[0].run()
         else:
             self.tx(0)
             self.rx(0)

@@ -23,6 +23,9 @@
  *   modem_rx_*               demodulator.rs:7-56     Demodulator::new(Carrier, S, Fn()->
  *                                                     FIRFilter) + Iterator<Item=(f32,f32)>
  *   modem_fir_*              fir.rs:3-35             FIRFilter::new(&[f32]) + add(f32)->f32
+ *   modem_chain_*            modulator.rs:85-100 then  one period of the sample-buffer loop:
+ *                            demodulator.rs:44-56      the DigitalModulator's samples of a bit
+ *                                                      buffer, then the Demodulator over them
  *
  * Conventions
  *   - Every function returns modem_status (0 = OK, negative = error) and never aborts.
@@ -51,8 +54,8 @@ extern "C" {
 
 /* 2: modem_tx_desc.q_offset; 3: the channel-batch entry points; 4: modem_rx_desc.phase_offset
  * (the descriptor grew 8 bytes: 80 -> 88), modem_pll_lock, MODEM_DTYPE_I16 and
- * MODEM_MIX_REFERENCE_REAL_EXACT. Layouts: INTEGRATION.md. */
-#define MODEM_HIP_ABI_VERSION 4
+ * MODEM_MIX_REFERENCE_REAL_EXACT; 5: modem_chain_* (no layout change). Layouts: INTEGRATION.md. */
+#define MODEM_HIP_ABI_VERSION 5
 
 typedef enum {
     MODEM_OK = 0,
@@ -254,6 +257,21 @@ modem_status modem_rx_flush(modem_rx* h, void* out_iq, uint8_t* out_sym, size_t 
                             size_t* produced, void* stream);
 uint64_t modem_rx_sample(const modem_rx* h);
 modem_status modem_rx_destroy(modem_rx* h);
+
+/* ---- One TX -> RX period over fixed device buffers ------------------------------------- */
+/* A prepared step of the sample-buffer loop: modem_chain_run(c) equals
+ *   modem_tx_process(tx, bits, nbits, samples, cap, &n, stream);
+ *   modem_rx_process(rx, samples, n, out_iq, out_sym, out_cap, &k, stream);
+ * (produced = n, produced_out = k), with the buffers checked once by modem_chain_create:
+ * device memory of the handles' one device (else INVALID_ARG); the TX writes interleaved
+ * complex samples (MODEM_OUT_IQ_MIXED or BASEBAND) of the RX's in_dtype. The handles stay
+ * usable on their own; the plan keeps pointers to them and to the buffers (destroy it first). */
+typedef struct modem_chain modem_chain;
+modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits, size_t nbits,
+                                void* samples, size_t cap, void* out_iq, uint8_t* out_sym,
+                                size_t out_cap, modem_chain** out);
+modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_out, void* stream);
+modem_status modem_chain_destroy(modem_chain* c);
 
 /* Demodulator::lock_phase (demodulator.rs:32-36): PLL::handle (pll.rs:16-22) over the n
  * complex samples x_iq (host memory; the reference uses n = 64), with the carrier phases of

@@ -161,9 +161,17 @@ def load_library():
         "modem_fir_process": (st, [vp, vp, vp, sz, vp]),
         "modem_fir_destroy": (st, [vp]),
         "modem_prng_bits": (st, [u64, vp, sz, c.c_int, vp]),
+        "modem_chain_create": (st, [vp, vp, vp, sz, vp, sz, vp, vp, sz, c.POINTER(vp)]),
+        "modem_chain_run": (st, [vp, c.POINTER(sz), c.POINTER(sz), vp]),
+        "modem_chain_destroy": (st, [vp]),
     }
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        try:
+            fn = getattr(L, name)
+        except AttributeError:
+            if name.startswith("modem_chain_"):   # ABI 5; experiment builds of older sources lack it
+                continue
+            raise
         fn.restype, fn.argtypes = res, args
     _lib = L
     return L
@@ -922,6 +930,47 @@ class RxBatchPlan:
             r._consumed += k
             r.carrier.sample = int(L.modem_rx_sample(r._h))
         return list(self._prod)
+
+
+class ChainPlan:
+    """One period of the sample-buffer loop as one C call (modem_chain_*): `run()` equals
+    `tx.process(bits, out=samples)` followed by `rx.process(samples, out_iq=out_iq,
+    out_sym=out_sym)` — the DigitalModulator's samples of the bit buffer (modulator.rs:85-100),
+    then the Demodulator over them (demodulator.rs:44-56) — with the device buffers checked once
+    here instead of on every call. Both handles' Python-side state (carried bits, carrier
+    sample, consumed samples) advances as those calls would advance it."""
+
+    def __init__(self, tx: "DigitalModulator", rx: "DemodulatorRx", bits, samples, out_iq=None, out_sym=None):
+        self.tx, self.rx = tx, rx
+        self.bits, self.samples, self.out_iq, self.out_sym = bits, samples, out_iq, out_sym
+        if tx.dtype != rx.in_dtype or tx.out_mode == OUT_REAL:
+            raise ValueError("ChainPlan: the RX must read the TX's interleaved samples (one dtype)")
+        self._nbits = int(bits.numel() if _is_torch(bits) else bits.size)
+        caps = [int(x.shape[0]) for x in (out_iq, out_sym) if x is not None]
+        h = ctypes.c_void_p()
+        _check(load_library().modem_chain_create(tx._h, rx._h, _ptr(bits), self._nbits, _ptr(samples),
+                                                 int(samples.shape[0]), _ptr(out_iq) or None, _ptr(out_sym) or None,
+                                                 min(caps) if caps else 1 << 62, ctypes.byref(h)), "ChainPlan")
+        self._h = h
+        self._n, self._k = ctypes.c_size_t(), ctypes.c_size_t()
+        self._pn, self._pk = ctypes.byref(self._n), ctypes.byref(self._k)
+        self._fn = load_library().modem_chain_run
+
+    def run(self, stream=None):
+        """Returns (samples produced, kept instants produced)."""
+        _check(self._fn(self._h, self._pn, self._pk, _stream_handle(stream, self.tx.device)), "ChainPlan.run")
+        n = self._n.value
+        tx, rx = self.tx, self.rx
+        tx._ncarry = (tx._ncarry + self._nbits) % tx.bps
+        tx.carrier.sample += n
+        rx._consumed += n
+        rx.carrier.sample += n
+        return n, self._k.value
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.modem_chain_destroy(self._h)
+            self._h = None
 
 
 def prng_bits(seed: int, nbits: int, device: int = 0, stream=None):

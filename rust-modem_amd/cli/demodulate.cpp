@@ -14,10 +14,21 @@
 // and MODEM_DTYPE_I16 (glibc-exact cos / sin, the FIRFilter fold), formatting as Rust's f32
 // Display (fmt_f32.h). -b is accepted and unused, as in the reference. Panics of the reference
 // (an unknown option, fewer than 64 samples for the lock) exit with status 101.
+//
+// Streaming, as the reference's iterator chain is: stdin is read as Rust's Stdin reads it (a
+// BufReader of 8 KiB that refills with one read(2) only when empty, and a two-byte read that
+// gets one byte ends the stream: bin/util.rs:13-24), the samples of each refill (several
+// refills while more input is already waiting, up to kChunk samples) go through
+// modem_rx_process, and their lines are written and flushed before the next read blocks — a
+// live pipe sees its lines as its samples arrive, and memory stays bounded.
 #include "../../include/modem_hip.h"
 #include "demod_taps.h"
 #include "fmt_f32.h"
 
+#include <poll.h>
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -44,14 +55,50 @@ void check(modem_status s, const char* what) {
     std::exit(3);
 }
 
-std::vector<int16_t> read_stdin_i16() {
-    std::vector<unsigned char> bytes;
-    unsigned char buf[1 << 16];
-    size_t got;
-    while ((got = std::fread(buf, 1, sizeof buf, stdin)) > 0) bytes.insert(bytes.end(), buf, buf + got);
-    std::vector<int16_t> x(bytes.size() / 2);
-    if (!x.empty()) std::memcpy(x.data(), bytes.data(), x.size() * 2);   // std::mem::transmute: native endian
-    return x;
+// Rust's Stdin as bin/util.rs reads it: an 8 KiB BufReader (refilled by one read(2) when it is
+// empty) and read_i16, whose two-byte read ends the stream when it gets fewer than two bytes.
+struct StdinI16 {
+    unsigned char buf[8192];
+    size_t pos = 0, len = 0;
+    bool done = false;
+    // One refill's worth of samples appended to `out` (false: the stream has ended).
+    bool refill(std::vector<int16_t>& out) {
+        if (done) return false;
+        ssize_t k;
+        do k = ::read(0, buf, sizeof buf); while (k < 0 && errno == EINTR);
+        if (k <= 0) { done = true; return false; }
+        len = (size_t)k;
+        pos = 0;
+        const size_t ns = len / 2;
+        const size_t at = out.size();
+        out.resize(at + ns);
+        if (ns) std::memcpy(out.data() + at, buf, ns * 2);   // std::mem::transmute: native endian
+        pos = ns * 2;
+        if (pos < len) done = true;                          // one byte left: Ok(1) -> end of input
+        return ns > 0 || !done;
+    }
+    // More input can be read without blocking.
+    static bool ready() {
+        pollfd p{0, POLLIN, 0};
+        return ::poll(&p, 1, 0) > 0 && (p.revents & (POLLIN | POLLHUP));
+    }
+};
+
+void print_lines(const float* iq, size_t n, std::vector<char>& out) {
+    char line[160];
+    for (size_t k = 0; k < n; ++k) {
+        int m = 0;
+        std::memcpy(line, "i:", 2); m = 2;
+        m += fmt_f32(line + m, iq[2 * k]);
+        std::memcpy(line + m, "\tq:", 3); m += 3;
+        m += fmt_f32(line + m, iq[2 * k + 1]);
+        line[m++] = '\n';
+        out.insert(out.end(), line, line + m);
+        if (out.size() > ((size_t)1 << 20)) { std::fwrite(out.data(), 1, out.size(), stdout); out.clear(); }
+    }
+    std::fwrite(out.data(), 1, out.size(), stdout);
+    out.clear();
+    std::fflush(stdout);
 }
 
 }  // namespace
@@ -71,7 +118,9 @@ int main(int argc, char** argv) {
             panic(std::string("called `Result::unwrap()` on an `Err` value: UnrecognizedOption(\"") + (a + 1) + "\")");
         }
     }
-    const std::vector<int16_t> x = read_stdin_i16();
+    StdinI16 in;
+    std::vector<int16_t> x;
+    while (x.size() < kLock && in.refill(x)) {}
     if (x.size() < kLock) panic("called `Option::unwrap()` on a `None` value");   // lock_phase
     const float w = modem_freq_sample_freq(kCarrier, kSampleRate);
 
@@ -101,26 +150,23 @@ int main(int argc, char** argv) {
     d.phase_offset = offset;
     modem_rx* rx;
     check(modem_rx_create(&d, 0, &rx), "rx");
-    std::vector<float> iq(2 * std::min(kChunk, x.size()));
+    x.erase(x.begin(), x.begin() + kLock);
+    std::vector<float> iq;
     std::vector<char> out;
     out.reserve((size_t)1 << 20);
-    char line[160];
-    for (size_t pos = kLock; pos < x.size(); pos += kChunk) {
-        const size_t n = std::min(kChunk, x.size() - pos);
-        size_t got = 0;
-        check(modem_rx_process(rx, x.data() + pos, n, iq.data(), nullptr, n, &got, nullptr), "rx");
-        for (size_t k = 0; k < got; ++k) {
-            int m = 0;
-            std::memcpy(line, "i:", 2); m = 2;
-            m += fmt_f32(line + m, iq[2 * k]);
-            std::memcpy(line + m, "\tq:", 3); m += 3;
-            m += fmt_f32(line + m, iq[2 * k + 1]);
-            line[m++] = '\n';
-            out.insert(out.end(), line, line + m);
-            if (out.size() > ((size_t)1 << 20)) { std::fwrite(out.data(), 1, out.size(), stdout); out.clear(); }
+    for (;;) {
+        // what is already waiting joins this call (bounded), then the call's lines go out
+        while (x.size() < kChunk && StdinI16::ready() && in.refill(x)) {}
+        if (!x.empty()) {
+            const size_t n = x.size();
+            iq.resize(2 * n);
+            size_t got = 0;
+            check(modem_rx_process(rx, x.data(), n, iq.data(), nullptr, n, &got, nullptr), "rx");
+            print_lines(iq.data(), got, out);
+            x.clear();
         }
+        if (!in.refill(x) && x.empty()) break;               // blocks until input or EOF
     }
-    std::fwrite(out.data(), 1, out.size(), stdout);
     check(modem_rx_destroy(rx), "rx");
     return 0;
 }

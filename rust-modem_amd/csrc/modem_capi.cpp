@@ -601,6 +601,30 @@ static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool 
     p.ph_max = h->ph_max;
 }
 
+// The kernel launch of one TX call on device buffers and the handle's state update.
+static modem_status tx_launch(modem_tx* h, const uint8_t* dbits, size_t nbits, bool flush, void* dout, int64_t nsym,
+                              int ncarry_new, size_t nsamp, hipStream_t s) {
+    modem_status st;
+    mk::TxParams p{};
+    tx_fill(h, dbits, nbits, flush, dout, nsym, ncarry_new, nsamp, p);
+    p.scan = nullptr;
+    if (phasor_scanned(h->ph_kind)) {
+        if ((st = h->scan_stage.ensure((size_t)std::max<int64_t>(nsym, 1) * sizeof(float2)))) return st;
+        p.scan = static_cast<float2*>(h->scan_stage.p);
+    }
+    if (h->ph_kind)
+        HIP_TRY(mk::launch_tx_phasor(p, h->dtype, h->out_mode, s));
+    else if (h->mfma_ksteps > 0)
+        HIP_TRY(mk::launch_tx_mfma(p, (int)h->sps, h->mfma_ksteps, h->d_bfrag, h->dtype, h->out_mode, s));
+    else
+        HIP_TRY(mk::launch_tx(p, (int)h->sps, h->dtype, h->out_mode, s));
+    h->hcur ^= 1;
+    if (!flush) { h->ccur ^= 1; h->ncarry = ncarry_new; }
+    h->sample += nsamp;
+    h->symbols += (uint64_t)nsym;
+    return MODEM_OK;
+}
+
 static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool flush, void* out,
                            size_t cap, size_t* produced, hipStream_t s) {
     if (!h || !produced || (nbits && !bits)) return MODEM_ERR_INVALID_ARG;
@@ -630,23 +654,7 @@ static modem_status tx_run(modem_tx* h, const uint8_t* bits, size_t nbits, bool 
         if ((st = h->out_stage.ensure(nsamp * tx_sample_bytes(h)))) return st;
         dout = h->out_stage.p;
     }
-    mk::TxParams p{};
-    tx_fill(h, dbits, nbits, flush, dout, nsym, ncarry_new, nsamp, p);
-    p.scan = nullptr;
-    if (phasor_scanned(h->ph_kind)) {
-        if ((st = h->scan_stage.ensure((size_t)std::max<int64_t>(nsym, 1) * sizeof(float2)))) return st;
-        p.scan = static_cast<float2*>(h->scan_stage.p);
-    }
-    if (h->ph_kind)
-        HIP_TRY(mk::launch_tx_phasor(p, h->dtype, h->out_mode, s));
-    else if (h->mfma_ksteps > 0)
-        HIP_TRY(mk::launch_tx_mfma(p, (int)h->sps, h->mfma_ksteps, h->d_bfrag, h->dtype, h->out_mode, s));
-    else
-        HIP_TRY(mk::launch_tx(p, (int)h->sps, h->dtype, h->out_mode, s));
-    h->hcur ^= 1;
-    if (!flush) { h->ccur ^= 1; h->ncarry = ncarry_new; }
-    h->sample += nsamp;
-    h->symbols += (uint64_t)nsym;
+    if ((st = tx_launch(h, dbits, nbits, flush, dout, nsym, ncarry_new, nsamp, s))) return st;
     if (host_out) {
         HIP_TRY(hipMemcpyAsync(out, dout, nsamp * tx_sample_bytes(h), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -912,6 +920,21 @@ static void rx_fill(const modem_rx* h, const void* din, size_t n, void* diq, uin
     p.tap_scale_exp = h->tap_scale_exp;
 }
 
+// The kernel launch of one RX call on device buffers and the handle's state update.
+static modem_status rx_launch(modem_rx* h, const void* din, size_t n, void* diq, uint8_t* dsym, int64_t k_first,
+                              int64_t nout, hipStream_t s) {
+    mk::RxParams p{};
+    rx_fill(h, din, n, diq, dsym, k_first, nout, p);
+    if (h->mfma_ksteps > 0) {
+        HIP_TRY(mk::launch_rx_mfma(p, (int)h->decim, h->mfma_ksteps, h->d_bfrag, h->in_dtype, h->out_dtype,
+                                   h->mix, s));
+    } else
+        HIP_TRY(mk::launch_rx(p, (int)h->decim, h->in_dtype, h->out_dtype, h->mix, s));
+    h->hcur ^= 1;
+    h->consumed += (int64_t)n;
+    return MODEM_OK;
+}
+
 static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, void* out_iq,
                            uint8_t* out_sym, size_t cap, size_t* produced, hipStream_t s) {
     if (!h || !produced || (n && !in && !zeros)) return MODEM_ERR_INVALID_ARG;
@@ -944,15 +967,7 @@ static modem_status rx_run(modem_rx* h, const void* in, size_t n, bool zeros, vo
         if ((st = h->sym_stage.ensure((size_t)nout))) return st;
         dsym = static_cast<uint8_t*>(h->sym_stage.p);
     }
-    mk::RxParams p{};
-    rx_fill(h, din, n, diq, dsym, k_first, nout, p);
-    if (h->mfma_ksteps > 0)
-        HIP_TRY(mk::launch_rx_mfma(p, (int)h->decim, h->mfma_ksteps, h->d_bfrag, h->in_dtype, h->out_dtype,
-                                   h->mix, s));
-    else
-        HIP_TRY(mk::launch_rx(p, (int)h->decim, h->in_dtype, h->out_dtype, h->mix, s));
-    h->hcur ^= 1;
-    h->consumed += (int64_t)n;
+    if ((st = rx_launch(h, din, n, diq, dsym, k_first, nout, s))) return st;
     if (host_iq) HIP_TRY(hipMemcpyAsync(out_iq, diq, (size_t)nout * rx_out_bytes(h), hipMemcpyDeviceToHost, s));
     if (host_sym) HIP_TRY(hipMemcpyAsync(out_sym, dsym, (size_t)nout, hipMemcpyDeviceToHost, s));
     if (host_iq || host_sym || din == h->in_stage.p) HIP_TRY(hipStreamSynchronize(s));
@@ -1030,6 +1045,69 @@ modem_status modem_rx_process_batch(modem_rx* const* hs, size_t nch, const void*
 }
 uint64_t modem_rx_sample(const modem_rx* h) { return h ? h->c0 + (uint64_t)h->consumed : 0; }
 modem_status modem_rx_destroy(modem_rx* h) { delete h; return MODEM_OK; }
+
+// ---------------------------------------------------------------------------- chain ----
+// A prepared TX -> RX step over fixed device buffers: the buffers' kinds are checked once here,
+// so a step is the two launches and the state updates (tx_run / rx_run minus the pointer
+// queries and staging decisions, ~1 us of host time each per call).
+struct modem_chain {
+    modem_tx* tx = nullptr;
+    modem_rx* rx = nullptr;
+    const uint8_t* bits = nullptr;
+    size_t nbits = 0;
+    void* samples = nullptr;
+    size_t cap = 0;
+    void* out_iq = nullptr;
+    uint8_t* out_sym = nullptr;
+    size_t out_cap = 0;
+};
+
+modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits, size_t nbits, void* samples,
+                                size_t cap, void* out_iq, uint8_t* out_sym, size_t out_cap, modem_chain** out) {
+    if (!tx || !rx || !out || !samples || (nbits && !bits)) return MODEM_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (tx->device != rx->device) return MODEM_ERR_INVALID_ARG;
+    // the RX reads what the TX writes: interleaved complex samples of one dtype
+    if (tx->out_mode == MODEM_OUT_REAL || rx->in_dtype != tx->dtype) return MODEM_ERR_INVALID_ARG;
+    const int dev = tx->device;
+    if ((nbits && ptr_kind(bits, dev) != PTR_DEVICE) || ptr_kind(samples, dev) != PTR_DEVICE ||
+        (out_iq && ptr_kind(out_iq, dev) != PTR_DEVICE) || (out_sym && ptr_kind(out_sym, dev) != PTR_DEVICE))
+        return MODEM_ERR_INVALID_ARG;
+    modem_chain* c = new (std::nothrow) modem_chain;
+    if (!c) return MODEM_ERR_ALLOC;
+    c->tx = tx; c->rx = rx; c->bits = bits; c->nbits = nbits; c->samples = samples; c->cap = cap;
+    c->out_iq = out_iq; c->out_sym = out_sym; c->out_cap = out_cap;
+    *out = c;
+    return MODEM_OK;
+}
+
+modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_out, void* stream) {
+    if (!c || !produced || !produced_out) return MODEM_ERR_INVALID_ARG;
+    *produced = *produced_out = 0;
+    modem_tx* tx = c->tx;
+    modem_rx* rx = c->rx;
+    const hipStream_t s = (hipStream_t)stream;
+    const uint64_t total = (uint64_t)tx->ncarry + c->nbits;
+    const int64_t nsym = (int64_t)(total / tx->bps);
+    const int ncarry_new = (int)(total - (uint64_t)nsym * tx->bps);
+    const size_t nsamp = (size_t)nsym * tx->sps;
+    if (nsamp > c->cap) return MODEM_ERR_CAPACITY;
+    int64_t k_first, nout;
+    rx_range(rx->consumed, rx->consumed + (int64_t)nsamp, rx->decim, rx->D, &k_first, &nout);
+    if ((size_t)nout > c->out_cap) return MODEM_ERR_CAPACITY;
+    DeviceGuard g(tx->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_status st;
+    if ((st = tx_launch(tx, c->bits, c->nbits, false, c->samples, nsym, ncarry_new, nsamp, s))) return st;
+    if ((st = rx_launch(rx, c->samples, nsamp, nout ? c->out_iq : nullptr, nout ? c->out_sym : nullptr, k_first,
+                        nout, s)))
+        return st;
+    *produced = nsamp;
+    *produced_out = (size_t)nout;
+    return MODEM_OK;
+}
+
+modem_status modem_chain_destroy(modem_chain* c) { delete c; return MODEM_OK; }
 
 // ----------------------------------------------------------------------------- FIR ----
 struct modem_fir {

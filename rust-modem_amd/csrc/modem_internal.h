@@ -93,7 +93,7 @@ struct RxParams {
     float phase_offset;      // PLL offset added to the carrier phase (demodulator.rs:50)
     int32_t idx46;           // every carrier index of this call is < 2^46 (rx_mfma's f32 index split)
     const int* ka_in;        // rx_mfma: staging exponent the previous call ended with (INT_MIN: none)
-    int* ka_out;             // rx_mfma: the one this call ends with (workgroup 0's last tile)
+    int* ka_out;             // rx_mfma: the one this call ends with (written with its last tile)
 };
 
 struct FirParams {

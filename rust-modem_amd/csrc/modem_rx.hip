@@ -68,6 +68,23 @@ template <> struct InIO<int16_t> {
     }
 };
 
+// Diagnostic builds only (-DMODEM_STAMPS, tools/stamps.py): s_memtime per wave at the phase
+// boundaries of each tile, stored by lane 0 (a vector store) into a buffer nothing else reads.
+// Layout [block * 4 + wave][tile slot 0..7][point 0..7]; tile slot 7 holds the wave's header
+// (entry / exit clocks, HW_ID, XCC_ID).
+#ifdef MODEM_STAMPS
+constexpr int kStampWaves = 8192, kStampTiles = 8, kStampPts = 8;
+__device__ unsigned long long g_modem_stamps[kStampWaves * kStampTiles * kStampPts];
+__device__ __forceinline__ void modem_stamp(int tile, int pt, unsigned long long v) {
+    const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && w < kStampWaves && tile < kStampTiles)
+        g_modem_stamps[((size_t)w * kStampTiles + tile) * kStampPts + pt] = v;
+}
+#define RX_STAMP(t, k) modem_stamp((int)(t), (k), __builtin_amdgcn_s_memtime())
+#else
+#define RX_STAMP(t, k) ((void)0)
+#endif
+
 enum { MIX_COMPLEX = 0, MIX_REFERENCE_REAL = 1, MIX_REFERENCE_REAL_EXACT = 2 };
 enum { SLICER_NONE = 0, SLICER_NEAREST = 1, SLICER_QAM_AXIS = 2 };
 
@@ -423,8 +440,9 @@ __device__ __forceinline__ int tile_ka(int ex) {
 }
 __device__ __forceinline__ int f32_exp(float m) { return (int)((__float_as_uint(m) >> 23) & 0xff); }
 
-// The tiles one workgroup runs, in order: first, first + step, ... (count of them).
-struct TileSeq { int64_t first, step, count; };
+// The tiles one workgroup runs, in order: first, first + step, ... (count of them), of the
+// call's ntiles.
+struct TileSeq { int64_t first, step, count, ntiles; };
 
 // Buffer descriptor over `bytes` bytes at `base` (wave-uniform inputs made provably uniform).
 // Accesses past `bytes` load zeros / are dropped without touching memory.
@@ -745,38 +763,54 @@ struct RxMfma {
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int64_t q_lo = q_lo_of(p, t), n_lo = q_lo + p.n_start;
         // 1. The window's raw samples into the planes' LDS (free until this tile is staged),
-        //    each through two buffer descriptors, one over the chunk and one over the history
-        //    (only a call's first tile reaches before the chunk): out of range loads return
-        //    zeros without a memory access, so the loads carry no branches and are all in
-        //    flight together.
+        //    through a buffer descriptor over the chunk (out of range loads return zeros without
+        //    a memory access, so they carry no branches), issued in batches of 8 per lane with
+        //    the LDS writes after each batch: the compiler otherwise waited for every load pair
+        //    before issuing the next (vmcnt(0) per sample), 17 round trips on C3 — the call's
+        //    first tile took 10-16 us against ~3.5 for a fast one (r03 stamps, tools/stamps.py).
+        //    The window's samples before the chunk (only a call's first tile has them) are then
+        //    patched in from the history.
         float2* raw = reinterpret_cast<float2*>(pl);
         {
             constexpr int S = sizeof(InT) * 2;
+            constexpr int NK = (NS + NT - 1) / NT, BATCH = 8;
             const int64_t ex = q_lo >= 0 ? 0 : -q_lo;                 // first window sample in the chunk
             const int64_t qx = q_lo + ex;
             const int64_t nx = p.N - qx < NS ? p.N - qx : NS;
             const __amdgpu_buffer_rsrc_t rx = buf_rsrc(reinterpret_cast<const char*>(p.x) + qx * S,
                                                        (uint32_t)(nx > 0 ? nx : 0) * S);
-            const int64_t hb = q_lo + p.HL;                           // history index of sample 0
-            const int64_t eh = hb >= 0 ? 0 : -hb;                     // first window sample in the history
-            const int64_t nhist = p.HL - (hb + eh);
-            const __amdgpu_buffer_rsrc_t rh = buf_rsrc(reinterpret_cast<const char*>(p.hist) + (hb + eh) * S,
-                                                       (uint32_t)(nhist > 0 ? nhist : 0) * S);
-            const int ox = (int)ex, oh = (int)eh;
+            const int ox = (int)ex;
+            auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+                if constexpr (std::is_same<InT, float>::value)
+                    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+                else
+                    return __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0)));
+            };
 #pragma unroll
-            for (int k = 0; k < (NS + NT - 1) / NT; ++k) {
-                const int e = tid + k * NT;
-                if ((k + 1) * NT > NS && e >= NS) break;
-                const uint32_t fx = (uint32_t)(e - ox) * S, fh = (uint32_t)(e - oh) * S;   // < 0: wraps, out of range
-                float2 v, w;
-                if constexpr (std::is_same<InT, float>::value) {
-                    v = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rx, fx, 0, 0));
-                    w = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rh, fh, 0, 0));
-                } else {
-                    v = __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(rx, fx, 0, 0)));
-                    w = __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(rh, fh, 0, 0)));
+            for (int k0 = 0; k0 < NK; k0 += BATCH) {
+                float2 v[BATCH];
+#pragma unroll
+                for (int b = 0; b < BATCH; ++b)       // < 0: wraps, out of range -> 0
+                    if (k0 + b < NK) v[b] = ld(rx, (uint32_t)(tid + (k0 + b) * NT - ox) * S);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < BATCH; ++b) {
+                    const int e = tid + (k0 + b) * NT;
+                    if (k0 + b < NK && ((k0 + b + 1) * NT <= NS || e < NS)) raw[e] = v[b];
                 }
-                raw[e] = e >= ox ? v : w;
+            }
+            if (ox > 0) {                                             // uniform: the call's first tile
+                const int64_t hb = q_lo + p.HL;                       // history index of sample 0
+                const int64_t eh = hb >= 0 ? 0 : -hb;                 // first window sample in the history
+                const int64_t nhist = p.HL - (hb + eh);
+                const __amdgpu_buffer_rsrc_t rh = buf_rsrc(reinterpret_cast<const char*>(p.hist) + (hb + eh) * S,
+                                                           (uint32_t)(nhist > 0 ? nhist : 0) * S);
+                const int oh = (int)eh;
+                for (int k = 0; k * NT < ox && k < NK; ++k) {         // uniform bounds
+                    const int e = tid + k * NT;
+                    const float2 w = ld(rh, (uint32_t)(e - oh) * S);
+                    if (e < ox && e < NS) raw[e] = w;
+                }
             }
         }
         __syncthreads();
@@ -850,11 +884,27 @@ struct RxMfma {
             // the staging (VALU-bound, the limiting stage) issues ahead of the other
             // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
             // event, +0.8 % bench (profiles/r02_store_layout_ab.txt; priority 3: no better)
+            RX_STAMP(i, 0);
             __builtin_amdgcn_s_setprio(1);
             stage<SC>(p, pl, votes, ix, sc, win, pre, nxt);
+#ifdef MODEM_RX_PAD_SNOP            // sensitivity builds only: extra scalar issue per tile
+#pragma unroll
+            for (int k = 0; k < MODEM_RX_PAD_SNOP; ++k) asm volatile("s_nop 0");
+#endif
+#ifdef MODEM_RX_PAD_VALU            // sensitivity builds only: extra vector issue per tile
+            {
+                float dv = (float)threadIdx.x;
+#pragma unroll
+                for (int k = 0; k < MODEM_RX_PAD_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(dv));
+                asm volatile("" :: "v"(dv));
+            }
+#endif
             __builtin_amdgcn_s_setprio(0);
+            RX_STAMP(i, 1);
             __syncthreads();
+            RX_STAMP(i, 2);
             if (!(fi && fast_ok(votes, kpred))) return;
+            if (t == sq.ntiles - 1 && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
             f32x4 dre, dim;
             if (NWF == NW || wave < NWF) {     // uniform
 #ifdef MODEM_RX_ABLATE_FIR          // profiling builds only: no matched filter
@@ -862,13 +912,16 @@ struct RxMfma {
 #else
                 fir(pl, tbl, dre, dim);
 #endif
+                RX_STAMP(i, 3);
 #ifdef MODEM_RX_ABLATE_STORE        // profiling builds only: no output stores
                 asm volatile("" :: "v"(dre[0] + dre[1] + dre[2] + dre[3] + dim[0] + dim[1] + dim[2] + dim[3]));
 #else
                 emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
 #endif
+                RX_STAMP(i, 4);
             }
             __syncthreads();                   // the planes are restaged next
+            RX_STAMP(i, 5);
             ++i;
         }
     }
@@ -877,6 +930,7 @@ struct RxMfma {
     __device__ static void run(const RxParams& p, _Float16* pl, _Float16* tbl, const _Float16* __restrict__ tables,
                                float* red, const TileSeq sq, int64_t bid) {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        RX_STAMP(7, 0);
         const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
         int* votes = reinterpret_cast<int*>(red);            // [4]
         float* reds = red + 4;                               // [4]
@@ -925,12 +979,22 @@ struct RxMfma {
             kpred = read_ka(reds);
             __syncthreads();
         }
+#ifdef MODEM_STAMPS
+        modem_stamp(7, 1, __builtin_amdgcn_s_memrealtime());
+        modem_stamp(7, 2, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
+        modem_stamp(7, 3, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
+        modem_stamp(7, 6, (unsigned long long)sq.first);
+#endif
         int64_t i = 0;
         while (i < sq.count) {
             if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
             else loop<true, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
             if (i < sq.count) {                // tile i on the general path (one place in the code)
-                kpred = slow_tile<EM>(p, pl, tbl, reds, sq.first + i * sq.step, cx.kb, cx.ld);
+                RX_STAMP(i, 6);
+                const int64_t ts = sq.first + i * sq.step;
+                kpred = slow_tile<EM>(p, pl, tbl, reds, ts, cx.kb, cx.ld);
+                if (ts == sq.ntiles - 1 && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
+                RX_STAMP(i, 7);
                 ++i;
                 // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
                 // not held across the general path, which has no registers to spare)
@@ -938,7 +1002,10 @@ struct RxMfma {
                 prefetch(t, i < sq.count && cx.full(p, t));
             }
         }
-        if (bid == 0 && threadIdx.x == 0) *p.ka_out = kpred;   // the next call's first prediction
+        RX_STAMP(7, 4);
+#ifdef MODEM_STAMPS
+        modem_stamp(7, 5, __builtin_amdgcn_s_memrealtime());
+#endif
     }
 };
 
@@ -960,8 +1027,12 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     // TX wrote last, each tile on the XCD slot that wrote it (blocks b and b + 8 share an XCD).
     // C3: 35.0 -> 33.8 us against contiguous ranges per workgroup; the same rounds with the
     // slots shifted by 1 or 4 measured 38.1-39.1 us (PMC FETCH_SIZE per launch unchanged).
+    if (ntiles <= 0) {                         // no tile: the next call predicts as this one did
+        if (bid == 0 && threadIdx.x == 0) *p.ka_out = *p.ka_in;
+        return;
+    }
     const int64_t R = (ntiles + nb - 1) / nb * nb;
-    TileSeq sq{R - nb + bid, -nb, R / nb};
+    TileSeq sq{R - nb + bid, -nb, R / nb, ntiles};
     if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }
     if (sq.count <= 0) return;
     K::template run<EM>(p, pl, tbl, tables, red, sq, bid);
@@ -1269,4 +1340,17 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
 
 
 }  // namespace mk
-
+#ifdef MODEM_STAMPS
+// Diagnostic builds only: copy (and optionally clear) the RX stamp buffer (tools/stamps.py).
+extern "C" int modem_debug_rx_stamps(void* dst, size_t bytes, int clear) {
+    const size_t n = sizeof(mk::g_modem_stamps);
+    if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(mk::g_modem_stamps), bytes < n ? bytes : n, 0,
+                                   hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (clear) {
+        void* a = nullptr;
+        if (hipGetSymbolAddress(&a, HIP_SYMBOL(mk::g_modem_stamps)) != hipSuccess) return -2;
+        if (hipMemset(a, 0, n) != hipSuccess) return -3;
+    }
+    return hipDeviceSynchronize() == hipSuccess ? (int)(n / 8) : -4;
+}
+#endif

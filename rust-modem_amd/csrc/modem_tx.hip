@@ -14,6 +14,23 @@
 
 namespace mk {
 
+// Diagnostic builds only (-DMODEM_STAMPS, tools/stamps.py --kernel tx): s_memtime per wave at the
+// phase boundaries of each TX tile (lane 0's vector store into a buffer nothing else reads).
+// Layout [block * 4 + wave][tile slot 0..7][point 0..7]; slot 7: entry / realtime / HW_ID / XCC_ID
+// / exit / realtime.
+#ifdef MODEM_STAMPS
+constexpr int kTxStampWaves = 8192, kTxStampTiles = 8, kTxStampPts = 8;
+__device__ unsigned long long g_modem_tx_stamps[kTxStampWaves * kTxStampTiles * kTxStampPts];
+__device__ __forceinline__ void modem_tx_stamp(int tile, int pt, unsigned long long v) {
+    const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && w < kTxStampWaves && tile < kTxStampTiles)
+        g_modem_tx_stamps[((size_t)w * kTxStampTiles + tile) * kTxStampPts + pt] = v;
+}
+#define TX_STAMP(t, k) modem_tx_stamp((int)(t), (k), __builtin_amdgcn_s_memtime())
+#else
+#define TX_STAMP(t, k) ((void)0)
+#endif
+
 // ---------------------------------------------------------------- symbol mapping (TX) ----
 // bytes_to_bits (digital/util.rs:5-11) of symbol m's bits, MSB first, `b & 1` per byte.
 __device__ __forceinline__ uint32_t tx_symbol_index(const TxParams& p, int64_t m) {
@@ -350,14 +367,32 @@ struct TxMfma {
         return (th4){rh, (_Float16)(r - (float)rh), ih, (_Float16)(i - (float)ih)};
     }
 
-    // General staging: first tile (history), leftover bits, flush, any bps.
-    __device__ static void stage_slow(const TxParams& p, _Float16* pl, int64_t ms) {
-        for (int e = threadIdx.x; e < NE; e += NT) {
+    // General staging: first tile (history), leftover bits, flush, any bps. Every lane's symbol
+    // indices (and history values) are loaded first, all in flight together, then looked up in
+    // the LDS copy of the split LUT (the same halves split_value gives the f32 LUT entry): the
+    // per-symbol form waited for each bits load and then for a global LUT load, ~10 serialized
+    // memory round trips per C3 tile.
+    __device__ static void stage_slow(const TxParams& p, _Float16* pl, const th4* lut_s, int64_t ms) {
+        constexpr int NK = (NE + NT - 1) / NT;
+        const int tid = threadIdx.x;
+        uint32_t idx[NK];
+        float2 hv[NK];
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int e = tid + k * NT;
             const int64_t m = ms + e;
-            float2 v;
-            if (m < 0) v = m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f);
-            else v = m >= p.nsym_valid ? make_float2(0.f, 0.f) : p.lut[tx_symbol_index(p, m)];
-            put(pl, e, split_value(p, v));
+            idx[k] = 0;
+            hv[k] = make_float2(0.f, 0.f);
+            if (e < NE) {
+                if (m < 0) { if (m >= -(int64_t)(p.K - 1)) hv[k] = p.hist[m + p.K - 1]; }
+                else if (m < p.nsym_valid) idx[k] = tx_symbol_index(p, m);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int e = tid + k * NT;
+            const int64_t m = ms + e;
+            if (e < NE) put(pl, e, m >= 0 && m < p.nsym_valid ? lut_s[idx[k]] : split_value(p, hv[k]));
         }
     }
 
@@ -510,22 +545,38 @@ struct TxMfma {
         int64_t t = t0;
         // the first tile's bits are requested before the LUT goes to LDS, so that the two
         // memory latencies at the kernel's start overlap
+        TX_STAMP(7, 0);
         bool ready = t < t1 && full(t);
         if (ready) prefetch(t);
         const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
         for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = lut_h[i];
         __syncthreads();   // LUT visible
+#ifdef MODEM_STAMPS
+        modem_tx_stamp(7, 1, __builtin_amdgcn_s_memrealtime());
+        modem_tx_stamp(7, 2, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
+        modem_tx_stamp(7, 3, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
+        int si = 0;
+#endif
         while (t < t1) {
             if (full(t)) {
                 if (!ready) prefetch(t);
                 ready = false;
                 for (; t < t1 && full(t); t += ts) {
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 0);
+#endif
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const int e = tid + NT * u;
                         if (e < NE) put(pl, e, lut_s[word_index(pre[u], BPS)]);
                     }
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 1);
+#endif
                     __syncthreads();
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 2);
+#endif
                     if (t + ts < t1) prefetch(t + ts);   // next bits fly during the MFMAs
                     const int64_t j0 = (t * TS - lead) * SPS;
 #pragma unroll
@@ -540,10 +591,20 @@ struct TxMfma {
                         emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                         __builtin_amdgcn_s_setprio(0);
                     }
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 4);
+#endif
                     __syncthreads();                     // the window is restaged next trip
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 5);
+                    ++si;
+#endif
                 }
             } else {
-                stage_slow(p, pl, t * TS - lead - PRE);
+#ifdef MODEM_STAMPS
+                TX_STAMP(si, 6);
+#endif
+                stage_slow(p, pl, lut_s, t * TS - lead - PRE);
                 __syncthreads();
                 const int64_t j0 = (t * TS - lead) * SPS;
 #pragma unroll 1
@@ -554,9 +615,17 @@ struct TxMfma {
                     emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                 }
                 __syncthreads();
+#ifdef MODEM_STAMPS
+                TX_STAMP(si, 7);
+                ++si;
+#endif
                 t += ts;
             }
         }
+        TX_STAMP(7, 4);
+#ifdef MODEM_STAMPS
+        modem_tx_stamp(7, 5, __builtin_amdgcn_s_memrealtime());
+#endif
     }
 };
 
@@ -930,3 +999,18 @@ hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStr
 
 
 }  // namespace mk
+
+#ifdef MODEM_STAMPS
+// Diagnostic builds only: copy (and optionally clear) the TX stamp buffer (tools/stamps.py).
+extern "C" int modem_debug_tx_stamps(void* dst, size_t bytes, int clear) {
+    const size_t n = sizeof(mk::g_modem_tx_stamps);
+    if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(mk::g_modem_tx_stamps), bytes < n ? bytes : n, 0,
+                                   hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (clear) {
+        void* a = nullptr;
+        if (hipGetSymbolAddress(&a, HIP_SYMBOL(mk::g_modem_tx_stamps)) != hipSuccess) return -2;
+        if (hipMemset(a, 0, n) != hipSuccess) return -3;
+    }
+    return hipDeviceSynchronize() == hipSuccess ? (int)(n / 8) : -4;
+}
+#endif

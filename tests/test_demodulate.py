@@ -144,6 +144,73 @@ def test_demodulate_cli_byte_exact(o, tmp_path, nbits, scale, tail):
     assert r.stdout == want, (len(r.stdout), len(want))
 
 
+def _read_lines(stream, n, timeout):
+    """Read n lines from a pipe within `timeout` s (None if they do not arrive)."""
+    import select
+    import time
+    buf = b""
+    end = time.time() + timeout
+    while buf.count(b"\n") < n:
+        left = end - time.time()
+        if left <= 0 or not select.select([stream], [], [], left)[0]:
+            return None
+        chunk = os.read(stream.fileno(), 1 << 16)
+        if not chunk:
+            break
+        buf += chunk
+    return buf
+
+
+@pytest.mark.gpu
+def test_demodulate_cli_streams(o):
+    """Lines come out as the samples go in (demodulate.rs:29-43 is an iterator chain): samples
+    written through a pipe in small writes produce their lines while stdin is still open, and
+    the whole output still equals the one-shot oracle text byte for byte."""
+    x = passband_i16(o, nbits=300, scale=12000.0)
+    want = expected_text(o, x)
+    p = subprocess.Popen([CLI], stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+    try:
+        head = 64 + 500
+        for a in range(0, head, 100):                       # 100-sample writes
+            p.stdin.write(x[a:min(a + 100, head)].tobytes())
+            p.stdin.flush()
+        got = _read_lines(p.stdout, 500, timeout=60)       # stdin is still open
+        assert got is not None, "no output before EOF: demodulate is not streaming"
+        p.stdin.write(x[head:].tobytes())
+        p.stdin.close()
+        rest = p.stdout.read()
+        assert p.wait(timeout=60) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert got + rest == want, (len(got + rest), len(want))
+
+
+@pytest.mark.gpu
+def test_demodulate_cli_odd_refill_ends_input(o):
+    """bin/util.rs:14-23 on Rust's 8 KiB-buffered Stdin: a refill that leaves one byte makes the
+    next two-byte read short, which ends the sample stream — later input is never read."""
+    x = passband_i16(o, nbits=300, scale=12000.0)
+    n0 = 64 + 300
+    p = subprocess.Popen([CLI], stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+    try:
+        p.stdin.write(x[:n0].tobytes() + b"\x07")           # one atomic write: an odd refill
+        p.stdin.flush()
+        got = _read_lines(p.stdout, n0 - 64, timeout=60)
+        assert got is not None
+        try:
+            p.stdin.write(x[n0:].tobytes())
+            p.stdin.close()
+        except BrokenPipeError:
+            pass
+        rest = p.stdout.read()
+        assert p.wait(timeout=60) == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+    assert got + rest == expected_text(o, x[:n0])
+
+
 @pytest.mark.gpu
 def test_demodulate_cli_panics_like_the_reference(tmp_path):
     """Fewer than 64 samples: lock_phase's unwrap panics (exit 101); an unknown option too."""

@@ -56,3 +56,20 @@ def test_two_ranks_real_kernels(tmp_path):
     total = (1 << 18) * 2 * 20 * world
     assert abs(outs[0]["value"] - total / (outs[0]["ms_per_step"] * 20 / 1e3) / 1e6) <= 0.02 * outs[0]["value"]
     assert not set(outs[0]["_seeds"]) & set(outs[1]["_seeds"])
+
+
+def test_bench_gpus_flag_two_ranks():
+    """`bench.py --gpus 2` without a launcher: two fresh rank processes (here both on the box's
+    one GPU, so the timing barrier runs over gloo; one GPU per rank uses RCCL), each running
+    config 4's 8-channel workload; rank 0's line reports the node size, every channel's
+    decisions on both ranks, and the host gather of the decisions timed apart from `value`."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    out = bench.main(["--gpus", "2", "--config", "c4", "--steps", "10", "--warmup", "3", "--no-cpu-baseline"])
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    assert out["decisions_match_sent"] is True
+    g = out["gather"]
+    assert g["bytes_per_gpu"] == 8 * ((1 << 22) // 4 - 16) and g["ms"] > 0
+    total = (1 << 22) * 8 * 10 * 2
+    assert abs(out["value"] - total / (out["ms_per_step"] * 10 / 1e3) / 1e6) <= 0.02 * out["value"]

@@ -429,3 +429,47 @@ def test_c_host_loopback():
     print(r.stdout, r.stderr)
     assert r.returncode == 0
     assert "0 wrong" in r.stdout
+
+
+@pytest.mark.parametrize("cfg,dtype", [("c3_qam16", 0), ("c2_qpsk", 0), ("c5_qam256", 1)])
+def test_chain_plan_equals_separate_calls(m, o, torch_cuda, cfg, dtype):
+    """modem_chain_run (ChainPlan: the bench's step) equals modem_tx_process followed by
+    modem_rx_process on separate handles, bit for bit, over three periods of a stream whose bit
+    buffer leaves a carry (bits not a multiple of the symbol size); the handles' carrier samples
+    advance alike, and the decisions of the last period equal the symbols sent."""
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS[cfg]
+    taps = m.rrc_taps(L, sps, 0.35)
+    w = w_quarter(o)
+    nsym = 3000
+    nb = nsym * bps + (1 if bps > 1 else 0)
+    hb = o.prng_bits(SEED + 300, nb)
+    bits = torch.from_numpy(hb).cuda()
+    tdt = torch.float16 if dtype else torch.float32
+
+    def mk():
+        tx = m.DigitalModulator(m.Carrier(w, 12345), product_phasor(m, name), sps, taps, dtype=dtype)
+        rx = m.DemodulatorRx(m.Carrier(w, 12345), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                             slicer=product_phasor(m, name).slicer(), in_dtype=dtype, out_dtype=dtype)
+        return tx, rx
+    (tx1, rx1), (tx2, rx2) = mk(), mk()
+    cap = (nb + bps) // bps * sps
+    y = torch.empty((cap, 2), dtype=tdt, device="cuda")
+    oiq = torch.empty((cap // sps + 1, 2), dtype=tdt, device="cuda")
+    osym = torch.empty(cap // sps + 1, dtype=torch.uint8, device="cuda")
+    plan = m.ChainPlan(tx2, rx2, bits, y, oiq, osym)
+    for rnd in range(3):
+        ys = tx1.process(bits)
+        riq, rsym = rx1.process(ys)
+        n, k = plan.run()
+        torch.cuda.synchronize()
+        assert n == ys.shape[0] and k == rsym.shape[0], (rnd, n, k)
+        assert torch.equal(y[:n], ys) and torch.equal(oiq[:k], riq) and torch.equal(osym[:k], rsym), rnd
+        assert tx2.carrier.sample == tx1.carrier.sample and rx2.carrier.sample == rx1.carrier.sample
+    # sanity: the decisions are the symbols of the (continuing) stream
+    stream_bits = np.concatenate([hb] * 3)
+    sent = sent_symbols(stream_bits[: (len(stream_bits) // bps) * bps], bps)
+    got = osym[:k].cpu().numpy()
+    c_prev = rx2.carrier.sample - 12345 - n                 # samples the RX consumed before the last call
+    k0 = max(0, -(-(c_prev - (L - 1)) // sps))              # its first kept instant (n = K sps + L - 1)
+    assert np.array_equal(got, sent[k0: k0 + k])

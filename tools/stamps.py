@@ -22,19 +22,22 @@ import bench  # noqa: E402
 W, T, P = 8192, 8, 8
 
 
-def grab(lib, clear):
+def grab(lib, clear, kernel="rx"):
     buf = np.zeros(W * T * P, dtype=np.uint64)
-    n = lib.modem_debug_rx_stamps(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes), int(clear))
+    fn = lib.modem_debug_rx_stamps if kernel == "rx" else lib.modem_debug_tx_stamps
+    n = fn(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes), int(clear))
     assert n > 0, n
     return buf.reshape(W, T, P)
 
 
-def summary(s, grid_waves):
+def summary(s, grid_waves, kernel="rx"):
     s = s[:grid_waves].astype(np.int64)
     hdr = s[:, 7]
     xcc = hdr[:, 3] & 0xF
     out = []
-    for name, a, b in (("stage", 0, 1), ("bar1", 1, 2), ("fir", 2, 3), ("emit", 3, 4), ("bar2", 4, 5)):
+    phases = (("stage", 0, 1), ("bar1", 1, 2), ("fir", 2, 3), ("emit", 3, 4), ("bar2", 4, 5)) if kernel == "rx" else \
+        (("stage", 0, 1), ("bar1", 1, 2), ("fir+emit", 2, 4), ("bar2", 4, 5))
+    for name, a, b in phases:
         d = s[:, :7, b] - s[:, :7, a]
         ok = (s[:, :7, a] > 0) & (s[:, :7, b] > 0)
         v = d[ok]
@@ -62,29 +65,30 @@ def main():
     ap.add_argument("--tag", default="base")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--warm", type=int, default=400)
+    ap.add_argument("--kernel", choices=["rx", "tx"], default="rx")
     a = ap.parse_args()
     r = bench.GpuRunner(bench.WORKLOADS[a.config], 0, 0)
     m = r._m
     lib = m.load_library()
-    lib.modem_debug_rx_stamps.restype = ctypes.c_int
+    getattr(lib, f"modem_debug_{a.kernel}_stamps").restype = ctypes.c_int
     for _ in range(a.warm):
         r.step()
     r.sync()
     runs = []
     for k in range(3):
-        grab(lib, True)
+        grab(lib, True, a.kernel)
         r.tx(0)
         r.rx(0)
         r.sync()
-        runs.append(grab(lib, False))
+        runs.append(grab(lib, False, a.kernel))
     s = np.stack(runs)
     hw = s[0, :, 7, 2]
     nw = int((hw != 0).sum())
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"stamps_{a.tag}.npz"), stamps=s[:, :max(nw, 1)])
+    np.savez_compressed(os.path.join(ROOT, "gpurun_out", f"stamps_{a.tag}_{a.kernel}.npz"), stamps=s[:, :max(nw, 1)])
     for k in range(s.shape[0]):
         print(f"== run {k} ({nw} waves)")
-        print(summary(s[k], nw))
+        print(summary(s[k], nw, a.kernel))
     print("ok", r.check())
 
 
