@@ -52,6 +52,23 @@ __device__ __forceinline__ cf2 phase_from_f2(float w, cf2 nf) {
     return x - p;
 }
 
+// The same for four indices: two independent packed pairs per step, so that no packed op reads
+// the result of the one right before it (gfx950 pads such a read with an s_nop).
+typedef float cf4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ cf4 phase_from_f4(float w, cf4 nf) {
+#pragma clang fp contract(off)
+    // -TWO_PI kept opaque: x + fl(f * -TWO_PI) == fl(x - fl(TWO_PI * f)) (negation is exact), and
+    // stays a packed add instead of being folded back into two scalar subtractions
+    float ntp = -kTwoPi;
+    asm("" : "+s"(ntp));
+    const cf4 x = nf * w;
+    const cf4 q0 = x * kRcp2Pi;
+    const cf4 r = __builtin_elementwise_fma(q0, (cf4){ntp, ntp, ntp, ntp}, x);
+    const cf4 q1 = __builtin_elementwise_fma(r, (cf4){kRcp2Pi, kRcp2Pi, kRcp2Pi, kRcp2Pi}, q0);
+    const cf4 f = (cf4){__builtin_floorf(q1.x), __builtin_floorf(q1.y), __builtin_floorf(q1.z), __builtin_floorf(q1.w)};
+    return x + f * ntp;
+}
+
 // `n as f32` with round-to-nearest-even. Below 2^53 (`exact_idx`, checked on the host per
 // call) the index is exact as an f64 and one v_cvt_f32_f64 rounds it once, as rustc's u64 -> f32
 // does; the hot loops keep a per-lane f64 index and add the per-sample offset in f64 (no

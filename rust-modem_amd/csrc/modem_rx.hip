@@ -453,6 +453,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uin
                                              __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// clamp(v, 0, cap) of a wave-uniform 64-bit value with 32-bit scalar ops on its halves (a
+// 64-bit compare would go through the vector unit: v_cmp_*_i64 from SGPR pairs).
+__device__ __forceinline__ uint32_t clamp64_u32(int64_t v, uint32_t cap) {
+    const int32_t hi = (int32_t)((uint64_t)v >> 32);
+    const uint32_t lo = (uint32_t)(uint64_t)v;
+    return hi < 0 ? 0u : hi > 0 ? cap : (lo < cap ? lo : cap);
+}
+
 // QAM-axis decisions for (re, im) at once (rx_slice's roundings, contract off), the scale and
 // offset on the packed pipe.
 __device__ __forceinline__ uint8_t rx_slice_qam2(const RxParams& p, float re, float im) {
@@ -574,8 +582,7 @@ struct RxMfma {
     // is unconditional.
     __device__ static __amdgpu_buffer_rsrc_t window_rsrc(const RxParams& p, int64_t q_lo, bool live) {
         constexpr int S = sizeof(InT) * 2;
-        const int64_t avail = p.N - q_lo;
-        const uint32_t w = avail < 4 * NQ ? (uint32_t)(avail > 0 ? avail : 0) : (uint32_t)(4 * NQ);
+        const uint32_t w = clamp64_u32(p.N - q_lo, (uint32_t)(4 * NQ));
         return buf_rsrc(reinterpret_cast<const char*>(p.x) + q_lo * S, live ? w * (uint32_t)S : 0u);
     }
     __device__ static QT load_slot(__amdgpu_buffer_rsrc_t r, int voff, int u) {
@@ -675,21 +682,18 @@ struct RxMfma {
             Q::split(pre[u], x);
             const int e0 = 4 * (tid + NT * u);
             const float bu = bl + (float)(4 * NT * u);
-            const cf2 nf0 = (bu + (cf2){0.f, 1.f}) + ix.a;            // exact, then one rounding
-            const cf2 nf1 = (bu + (cf2){2.f, 3.f}) + ix.a;
-            const cf2 rv0 = __builtin_elementwise_fma(phase_from_f2(p.w, nf0), (cf2){kRcp2Pi, kRcp2Pi}, (cf2){roff, roff});
-            const cf2 rv1 = __builtin_elementwise_fma(phase_from_f2(p.w, nf1), (cf2){kRcp2Pi, kRcp2Pi}, (cf2){roff, roff});
-            const cf2 sn2[2] = {(cf2){__builtin_amdgcn_sinf(rv0.x), __builtin_amdgcn_sinf(rv0.y)},
-                                (cf2){__builtin_amdgcn_sinf(rv1.x), __builtin_amdgcn_sinf(rv1.y)}};
-            const cf2 cs2[2] = {(cf2){__builtin_amdgcn_cosf(rv0.x), __builtin_amdgcn_cosf(rv0.y)},
-                                (cf2){__builtin_amdgcn_cosf(rv1.x), __builtin_amdgcn_cosf(rv1.y)}};
+            const cf4 nf = (bu + (cf4){0.f, 1.f, 2.f, 3.f}) + ix.a;   // exact, then one rounding
+            const cf4 rv = __builtin_elementwise_fma(phase_from_f4(p.w, nf), (cf4){kRcp2Pi, kRcp2Pi, kRcp2Pi, kRcp2Pi},
+                                                     (cf4){roff, roff, roff, roff});
+            const float sn[4] = {__builtin_amdgcn_sinf(rv.x), __builtin_amdgcn_sinf(rv.y),
+                                 __builtin_amdgcn_sinf(rv.z), __builtin_amdgcn_sinf(rv.w)};
+            const float cs[4] = {__builtin_amdgcn_cosf(rv.x), __builtin_amdgcn_cosf(rv.y),
+                                 __builtin_amdgcn_cosf(rv.z), __builtin_amdgcn_cosf(rv.w)};
             float zr[4], zi[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float sn = sn2[j / 2][j % 2], cs = cs2[j / 2][j % 2];
-                cf2 z;
-                if (MIX == MIX_REFERENCE_REAL) z = (cf2){x[j].x * cs, x[j].x * -sn};
-                else z = cmix((cf2){x[j].x, x[j].y}, (cf2){cs, sn});
+                cf2 z = MIX == MIX_REFERENCE_REAL ? (cf2){x[j].x * cs[j], x[j].x * -sn[j]}
+                                                  : cmix((cf2){x[j].x, x[j].y}, (cf2){cs[j], sn[j]});
                 if (SC) z = z * sc;
                 zr[j] = z.x;
                 zi[j] = z.y;
@@ -698,6 +702,8 @@ struct RxMfma {
                     asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j]), "v"(zi[j]));
             }
             if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, pos0 + u * SLOT_POS, zr, zi);
+            // (not hoisted above the mix: the slot's registers would be copied out first)
+            __builtin_amdgcn_sched_barrier(0);
             pre[u] = load_slot(nxt, voff, u);                  // the next tile's slot u, same registers
             __builtin_amdgcn_sched_barrier(0);                 // one quad's temporaries at a time
         }
@@ -723,10 +729,10 @@ struct RxMfma {
             }
             return;
         }
-        const int64_t ob = ot < 0 ? 0 : ot;
-        const int sh = (int)(ot - ob);                       // -15 .. 0
-        const int64_t left = p.nout - ob;
-        const uint32_t nk = left < 256 ? (uint32_t)(left > 0 ? left : 0) : 256u;
+        const bool neg = (int32_t)((uint64_t)ot >> 32) < 0;   // before the call's first instant
+        const int64_t ob = neg ? 0 : ot;
+        const int sh = neg ? (int)ot : 0;                    // -15 .. 0
+        const uint32_t nk = clamp64_u32(p.nout - ob, 256u);
         const __amdgpu_buffer_rsrc_t riq = buf_rsrc(reinterpret_cast<OutT*>(p.out_iq) + 2 * ob, nk * 2 * sizeof(OutT));
         const __amdgpu_buffer_rsrc_t rsy = buf_rsrc(p.out_sym + ob, nk);
         f32x4 re = dre, im = dim;
@@ -862,25 +868,60 @@ struct RxMfma {
     struct Ctx {
         bool fast;
         int kb, ld;
-        __device__ bool full(const RxParams& p, int64_t t) const {
-            return fast && q_lo_of(p, t) >= 0 && t * TS >= ld;
-        }
     };
 
-    // Tiles i .. while their staging exponent keeps its class (SC: nonzero). Returns at the end
-    // of the sequence, or after the barrier of a tile the general path must redo.
+    // The workgroup's tiles t_i = first + i * step (i < count, step = -grid: top-down), walked
+    // with running values so that a tile's scalar bookkeeping is a few adds, not 64-bit
+    // multiplies and compares (the RX is issue-bound: 100 extra s_nop per tile cost it ~1.3 us,
+    // profiles/r03_sensitivity.txt): the tile, its window offset q = q_lo_of(t), and the
+    // number of leading tiles on the fast path (q and t only decrease along the walk, so the
+    // tiles with q >= 0 and t * TS >= lead come first).
+    struct Walk {
+        int64_t t, q, step, dq, last;          // tile, q_lo_of(t), steps per tile, the call's last tile
+        int32_t i, count, nfull;               // position, tiles in the walk, leading full tiles
+        __device__ void next() { ++i; t += step; q += dq; }
+        __device__ bool full() const { return i < nfull; }
+        __device__ bool next_full() const { return i + 1 < nfull && i + 1 < count; }
+    };
+    __device__ static Walk walk(const RxParams& p, const TileSeq& sq, bool fast) {
+        Walk w;
+        w.t = sq.first;
+        w.step = sq.step;
+        w.dq = sq.step * (int64_t)(TS * DEC);
+        w.q = q_lo_of(p, sq.first);
+        w.last = sq.ntiles - 1;
+        w.i = 0;
+        w.count = (int32_t)sq.count;
+        w.nfull = 0;
+        if (fast) {                            // the smallest full tile: q_lo_of(t) >= 0, t * TS >= lead
+            const int64_t q0 = q_lo_of(p, 0);
+            int64_t tmin = q0 >= 0 ? 0 : (-q0 + TS * DEC - 1) / (TS * DEC);
+            if (lead(p) > 0 && tmin < 1) tmin = 1;
+            if (sq.first >= tmin) {
+                const int64_t n = (sq.first - tmin) / -sq.step + 1;
+                w.nfull = (int32_t)(n < sq.count ? n : sq.count);
+            }
+        }
+        return w;
+    }
+
+    // Tiles from w.i on while their staging exponent keeps its class (SC: nonzero). Returns
+    // at the end of the walk, or after the barrier of a tile the general path must redo.
     template <bool SC, int EM>
-    __device__ static void loop(const RxParams& p, _Float16* pl, const _Float16* tbl, int* votes, const TileSeq sq,
-                                const Ctx& cx, QT (&pre)[U], int64_t& i, int kpred) {
+    __device__ static void loop(const RxParams& p, _Float16* pl, const _Float16* tbl, int* votes, Walk& w,
+                                const Ctx& cx, QT (&pre)[U], int kpred) {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         const float sc = __builtin_ldexpf(1.0f, kpred);
         const cf2 win = window(kpred);
-        while (i < sq.count) {
-            const int64_t t = sq.first + i * sq.step;
-            const bool fi = cx.full(p, t);
-            const bool pf = i + 1 < sq.count && cx.full(p, t + sq.step);
-            const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? q_lo_of(p, t + sq.step) : 0, pf);
-            const Idx ix = idx_split(p.c0 + (uint64_t)(q_lo_of(p, t) + p.n_start));
+#ifdef MODEM_STAMPS
+        const int& i = w.i;
+#endif
+        while (w.i < w.count) {
+            const int64_t t = w.t;
+            const bool fi = w.full();
+            const bool pf = w.next_full();
+            const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? w.q + w.dq : 0, pf);
+            const Idx ix = idx_split(p.c0 + (uint64_t)(w.q + p.n_start));
             // the staging (VALU-bound, the limiting stage) issues ahead of the other
             // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
             // event, +0.8 % bench (profiles/r02_store_layout_ab.txt; priority 3: no better)
@@ -904,7 +945,7 @@ struct RxMfma {
             __syncthreads();
             RX_STAMP(i, 2);
             if (!(fi && fast_ok(votes, kpred))) return;
-            if (t == sq.ntiles - 1 && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
+            if (t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
             f32x4 dre, dim;
             if (NWF == NW || wave < NWF) {     // uniform
 #ifdef MODEM_RX_ABLATE_FIR          // profiling builds only: no matched filter
@@ -922,7 +963,7 @@ struct RxMfma {
             }
             __syncthreads();                   // the planes are restaged next
             RX_STAMP(i, 5);
-            ++i;
+            w.next();
         }
     }
 
@@ -932,11 +973,12 @@ struct RxMfma {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         RX_STAMP(7, 0);
         const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
+        Walk w = walk(p, sq, cx.fast);
         int* votes = reinterpret_cast<int*>(red);            // [4]
         float* reds = red + 4;                               // [4]
         QT pre[U];
-        auto prefetch = [&](int64_t t, bool live) {
-            const __amdgpu_buffer_rsrc_t r = window_rsrc(p, live ? q_lo_of(p, t) : 0, live);
+        auto prefetch = [&](int64_t q, bool live) {
+            const __amdgpu_buffer_rsrc_t r = window_rsrc(p, live ? q : 0, live);
             const int voff = 4 * tid_() * (int)sizeof(InT) * 2;
 #pragma unroll
             for (int u = 0; u < U; ++u) pre[u] = load_slot(r, voff, u);
@@ -951,8 +993,8 @@ struct RxMfma {
             const int j = tid_() + k * NT;
             if (j < K_TAB8) tv[k] = reinterpret_cast<const h8*>(tables)[j];
         }
-        const bool f0 = cx.full(p, sq.first);
-        prefetch(sq.first, f0);
+        const bool f0 = w.full();
+        prefetch(w.q, f0);
 #pragma unroll
         for (int k = 0; k < NTB; ++k) {
             const int j = tid_() + k * NT;
@@ -984,22 +1026,20 @@ struct RxMfma {
         modem_stamp(7, 2, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
         modem_stamp(7, 3, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
         modem_stamp(7, 6, (unsigned long long)sq.first);
+        const int& i = w.i;
 #endif
-        int64_t i = 0;
-        while (i < sq.count) {
-            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
-            else loop<true, EM>(p, pl, tbl, votes, sq, cx, pre, i, kpred);
-            if (i < sq.count) {                // tile i on the general path (one place in the code)
+        while (w.i < w.count) {
+            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
+            else loop<true, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
+            if (w.i < w.count) {               // tile w.t on the general path (one place in the code)
                 RX_STAMP(i, 6);
-                const int64_t ts = sq.first + i * sq.step;
-                kpred = slow_tile<EM>(p, pl, tbl, reds, ts, cx.kb, cx.ld);
-                if (ts == sq.ntiles - 1 && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
+                kpred = slow_tile<EM>(p, pl, tbl, reds, w.t, cx.kb, cx.ld);
+                if (w.t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
                 RX_STAMP(i, 7);
-                ++i;
+                w.next();
                 // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
                 // not held across the general path, which has no registers to spare)
-                const int64_t t = sq.first + i * sq.step;
-                prefetch(t, i < sq.count && cx.full(p, t));
+                prefetch(w.q, w.i < w.count && w.full());
             }
         }
         RX_STAMP(7, 4);
