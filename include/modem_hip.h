@@ -54,7 +54,8 @@ extern "C" {
 
 /* 2: modem_tx_desc.q_offset; 3: the channel-batch entry points; 4: modem_rx_desc.phase_offset
  * (the descriptor grew 8 bytes: 80 -> 88), modem_pll_lock, MODEM_DTYPE_I16 and
- * MODEM_MIX_REFERENCE_REAL_EXACT; 5: modem_chain_* (no layout change). Layouts: INTEGRATION.md. */
+ * MODEM_MIX_REFERENCE_REAL_EXACT; 5: modem_chain_* (no layout change; modem_chain_fused
+ * added later, additive). Layouts: INTEGRATION.md. */
 #define MODEM_HIP_ABI_VERSION 5
 
 typedef enum {
@@ -271,6 +272,10 @@ modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits,
                                 void* samples, size_t cap, void* out_iq, uint8_t* out_sym,
                                 size_t out_cap, modem_chain** out);
 modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_out, void* stream);
+/* How the last modem_chain_run ran: 1 = one launch (the TX and RX of the period fused: the
+ * common filters, tile geometry permitting; results identical), 0 = the two launches, -1 = no
+ * run yet or c == NULL. MODEM_CHAIN_FUSED=0 in the environment at create time forces 0. */
+int modem_chain_fused(const modem_chain* c);
 modem_status modem_chain_destroy(modem_chain* c);
 
 /* Demodulator::lock_phase (demodulator.rs:32-36): PLL::handle (pll.rs:16-22) over the n

@@ -163,6 +163,7 @@ def load_library():
         "modem_prng_bits": (st, [u64, vp, sz, c.c_int, vp]),
         "modem_chain_create": (st, [vp, vp, vp, sz, vp, sz, vp, vp, sz, c.POINTER(vp)]),
         "modem_chain_run": (st, [vp, c.POINTER(sz), c.POINTER(sz), vp]),
+        "modem_chain_fused": (c.c_int, [vp]),
         "modem_chain_destroy": (st, [vp]),
     }
     for name, (res, args) in sig.items():
@@ -966,6 +967,11 @@ class ChainPlan:
         rx._consumed += n
         rx.carrier.sample += n
         return n, self._k.value
+
+    @property
+    def fused(self) -> int:
+        """1: the last run() was one launch (TX and RX of the period fused), 0: two, -1: none."""
+        return int(load_library().modem_chain_fused(self._h))
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -601,6 +602,14 @@ static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool 
     p.ph_max = h->ph_max;
 }
 
+// The handle's state after a TX call (the kernel wrote the other history / carry buffers).
+static void tx_advance(modem_tx* h, bool flush, int64_t nsym, int ncarry_new, size_t nsamp) {
+    h->hcur ^= 1;
+    if (!flush) { h->ccur ^= 1; h->ncarry = ncarry_new; }
+    h->sample += nsamp;
+    h->symbols += (uint64_t)nsym;
+}
+
 // The kernel launch of one TX call on device buffers and the handle's state update.
 static modem_status tx_launch(modem_tx* h, const uint8_t* dbits, size_t nbits, bool flush, void* dout, int64_t nsym,
                               int ncarry_new, size_t nsamp, hipStream_t s) {
@@ -618,10 +627,7 @@ static modem_status tx_launch(modem_tx* h, const uint8_t* dbits, size_t nbits, b
         HIP_TRY(mk::launch_tx_mfma(p, (int)h->sps, h->mfma_ksteps, h->d_bfrag, h->dtype, h->out_mode, s));
     else
         HIP_TRY(mk::launch_tx(p, (int)h->sps, h->dtype, h->out_mode, s));
-    h->hcur ^= 1;
-    if (!flush) { h->ccur ^= 1; h->ncarry = ncarry_new; }
-    h->sample += nsamp;
-    h->symbols += (uint64_t)nsym;
+    tx_advance(h, flush, nsym, ncarry_new, nsamp);
     return MODEM_OK;
 }
 
@@ -920,6 +926,12 @@ static void rx_fill(const modem_rx* h, const void* din, size_t n, void* diq, uin
     p.tap_scale_exp = h->tap_scale_exp;
 }
 
+// The handle's state after an RX call (the kernel wrote the other history / ka slot).
+static void rx_advance(modem_rx* h, size_t n) {
+    h->hcur ^= 1;
+    h->consumed += (int64_t)n;
+}
+
 // The kernel launch of one RX call on device buffers and the handle's state update.
 static modem_status rx_launch(modem_rx* h, const void* din, size_t n, void* diq, uint8_t* dsym, int64_t k_first,
                               int64_t nout, hipStream_t s) {
@@ -930,8 +942,7 @@ static modem_status rx_launch(modem_rx* h, const void* din, size_t n, void* diq,
                                    h->mix, s));
     } else
         HIP_TRY(mk::launch_rx(p, (int)h->decim, h->in_dtype, h->out_dtype, h->mix, s));
-    h->hcur ^= 1;
-    h->consumed += (int64_t)n;
+    rx_advance(h, n);
     return MODEM_OK;
 }
 
@@ -1048,9 +1059,14 @@ modem_status modem_rx_destroy(modem_rx* h) { delete h; return MODEM_OK; }
 
 // ---------------------------------------------------------------------------- chain ----
 // A prepared TX -> RX step over fixed device buffers: the buffers' kinds are checked once here,
-// so a step is the two launches and the state updates (tx_run / rx_run minus the pointer
+// so a step is one launch (modem_chain.hip: TX and RX of the period fused, where the filters
+// and the call's geometry allow; MODEM_CHAIN_FUSED=0 in the environment at create time turns
+// it off) or the two launches, and the state updates (tx_run / rx_run minus the pointer
 // queries and staging decisions, ~1 us of host time each per call).
 struct modem_chain {
+    bool fused = true;
+    int last = -1;             // how the last run ran (modem_chain_fused)
+    bool verbose = false;      // MODEM_CHAIN_VERBOSE=1: why a run took the two launches (stderr)
     modem_tx* tx = nullptr;
     modem_rx* rx = nullptr;
     const uint8_t* bits = nullptr;
@@ -1077,6 +1093,10 @@ modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits,
     if (!c) return MODEM_ERR_ALLOC;
     c->tx = tx; c->rx = rx; c->bits = bits; c->nbits = nbits; c->samples = samples; c->cap = cap;
     c->out_iq = out_iq; c->out_sym = out_sym; c->out_cap = out_cap;
+    const char* env = std::getenv("MODEM_CHAIN_FUSED");
+    c->fused = !(env && env[0] == '0');
+    const char* verb = std::getenv("MODEM_CHAIN_VERBOSE");
+    c->verbose = verb && verb[0] == '1';
     *out = c;
     return MODEM_OK;
 }
@@ -1098,14 +1118,43 @@ modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_
     DeviceGuard g(tx->device);
     if (!g.ok) return MODEM_ERR_NO_DEVICE;
     modem_status st;
+    const bool eligible = c->fused && !tx->ph_kind && tx->mfma_ksteps > 0 && rx->mfma_ksteps > 0 &&
+                          rx->mix == MODEM_MIX_COMPLEX && tx->out_mode == MODEM_OUT_IQ_MIXED &&
+                          rx->out_dtype == rx->in_dtype && tx->sps == rx->decim && nout > 0;
+    if (c->verbose && !eligible)
+        std::fprintf(stderr, "modem_chain_run: two launches (fused %d ph %d tx ks %d rx ks %d mix %d out_mode %d "
+                     "dtypes %d/%d sps %u decim %u nout %lld)\n", (int)c->fused, (int)tx->ph_kind, tx->mfma_ksteps,
+                     rx->mfma_ksteps, (int)rx->mix, (int)tx->out_mode, (int)rx->in_dtype, (int)rx->out_dtype,
+                     (unsigned)tx->sps, (unsigned)rx->decim, (long long)nout);
+    if (eligible) {
+        mk::TxParams tp{};
+        tx_fill(tx, c->bits, c->nbits, false, c->samples, nsym, ncarry_new, nsamp, tp);
+        mk::RxParams rp{};
+        rx_fill(rx, c->samples, nsamp, c->out_iq, c->out_sym, k_first, nout, rp);
+        const hipError_t e = mk::launch_chain_mfma(tp, (int)tx->sps, tx->mfma_ksteps, tx->d_bfrag, rp,
+                                                   rx->mfma_ksteps, rx->d_bfrag, tx->dtype, s);
+        if (e == hipSuccess) {
+            c->last = 1;
+            tx_advance(tx, false, nsym, ncarry_new, nsamp);
+            rx_advance(rx, nsamp);
+            *produced = nsamp;
+            *produced_out = (size_t)nout;
+            return MODEM_OK;
+        }
+        if (e != hipErrorNotSupported) { (void)hipGetLastError(); return MODEM_ERR_HIP; }
+        if (c->verbose) std::fprintf(stderr, "modem_chain_run: no fused form for this call (two launches)\n");
+    }
     if ((st = tx_launch(tx, c->bits, c->nbits, false, c->samples, nsym, ncarry_new, nsamp, s))) return st;
     if ((st = rx_launch(rx, c->samples, nsamp, nout ? c->out_iq : nullptr, nout ? c->out_sym : nullptr, k_first,
                         nout, s)))
         return st;
+    c->last = 0;
     *produced = nsamp;
     *produced_out = (size_t)nout;
     return MODEM_OK;
 }
+
+int modem_chain_fused(const modem_chain* c) { return c ? c->last : -1; }
 
 modem_status modem_chain_destroy(modem_chain* c) { delete c; return MODEM_OK; }
 

@@ -1,0 +1,936 @@
+// rust-modem_amd/csrc/modem_rx_mfma.h — the RX matched filter on the matrix cores (RxMfma,
+// rx_mfma_body) and the device helpers it shares with the other RX kernels: included by
+// modem_rx.hip (rx_mfma, rx_mfma_batch) and modem_chain.hip (the fused TX->RX period).
+#pragma once
+#include "modem_device.h"
+#include "libm_sincosf.h"
+
+namespace mk {
+
+// -------------------------------------------------------------------------------- RX ----
+template <typename InT> struct InIO;
+template <> struct InIO<float> {
+    using Raw = float4;   // two consecutive samples
+    __device__ static Raw load_raw(const void* x, int64_t q) {
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(x) + q);
+    }
+    __device__ static void split(Raw v, float2& a, float2& b) {
+        a = make_float2(v.x, v.y);
+        b = make_float2(v.z, v.w);
+    }
+    __device__ static float2 load(const void* x, int64_t q) {
+        return reinterpret_cast<const float2*>(x)[q];
+    }
+    __device__ static void load_pair(const void* x, int64_t q, float2& a, float2& b) {
+        const float4 v = *reinterpret_cast<const float4*>(reinterpret_cast<const float2*>(x) + q);
+        a = make_float2(v.x, v.y);
+        b = make_float2(v.z, v.w);
+    }
+    __device__ static void copy(void* dst, int64_t i, const void* src, int64_t q) {
+        reinterpret_cast<float2*>(dst)[i] = reinterpret_cast<const float2*>(src)[q];
+    }
+};
+template <> struct InIO<__half> {
+    using Raw = uint2;
+    __device__ static Raw load_raw(const void* x, int64_t q) {
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const __half2*>(x) + q);
+    }
+    __device__ static void split(Raw u, float2& a, float2& b) {
+        a = __half22float2(*reinterpret_cast<const __half2*>(&u.x));
+        b = __half22float2(*reinterpret_cast<const __half2*>(&u.y));
+    }
+    __device__ static float2 load(const void* x, int64_t q) {
+        return __half22float2(reinterpret_cast<const __half2*>(x)[q]);
+    }
+    __device__ static void load_pair(const void* x, int64_t q, float2& a, float2& b) {
+        const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const __half2*>(x) + q);
+        a = __half22float2(*reinterpret_cast<const __half2*>(&u.x));
+        b = __half22float2(*reinterpret_cast<const __half2*>(&u.y));
+    }
+    __device__ static void copy(void* dst, int64_t i, const void* src, int64_t q) {
+        reinterpret_cast<__half2*>(dst)[i] = reinterpret_cast<const __half2*>(src)[q];
+    }
+};
+
+// Real int16 samples (MODEM_DTYPE_I16, the `demodulate` reader): x = (v, 0).
+template <> struct InIO<int16_t> {
+    __device__ static float2 load(const void* x, int64_t q) {
+        return make_float2((float)reinterpret_cast<const int16_t*>(x)[q], 0.f);
+    }
+    __device__ static void copy(void* dst, int64_t i, const void* src, int64_t q) {
+        reinterpret_cast<int16_t*>(dst)[i] = reinterpret_cast<const int16_t*>(src)[q];
+    }
+};
+
+// Diagnostic builds only (-DMODEM_STAMPS, tools/stamps.py): s_memtime per wave at the phase
+// boundaries of each tile, stored by lane 0 (a vector store) into a buffer nothing else reads.
+// Layout [block * 4 + wave][tile slot 0..7][point 0..7]; tile slot 7 holds the wave's header
+// (entry / exit clocks, HW_ID, XCC_ID).
+#ifdef MODEM_STAMPS
+constexpr int kStampWaves = 8192, kStampTiles = 8, kStampPts = 8;
+static __device__ unsigned long long g_modem_stamps[kStampWaves * kStampTiles * kStampPts];
+__device__ __forceinline__ void modem_stamp(int tile, int pt, unsigned long long v) {
+    const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && w < kStampWaves && tile < kStampTiles)
+        g_modem_stamps[((size_t)w * kStampTiles + tile) * kStampPts + pt] = v;
+}
+#define RX_STAMP(t, k) modem_stamp((int)(t), (k), __builtin_amdgcn_s_memtime())
+#else
+#define RX_STAMP(t, k) ((void)0)
+#endif
+
+enum { MIX_COMPLEX = 0, MIX_REFERENCE_REAL = 1, MIX_REFERENCE_REAL_EXACT = 2 };
+enum { SLICER_NONE = 0, SLICER_NEAREST = 1, SLICER_QAM_AXIS = 2 };
+
+// Sample q of the chunk (q < 0: history; q >= N: past the chunk, zero).
+template <typename InT>
+__device__ __forceinline__ float2 rx_sample(const RxParams& p, int64_t q) {
+    if (q < -(int64_t)p.HL) return make_float2(0.f, 0.f);
+    if (q >= 0) return q < p.N ? InIO<InT>::load(p.x, q) : make_float2(0.f, 0.f);
+    return InIO<InT>::load(p.hist, q + p.HL);
+}
+
+template <typename InT>
+__device__ __forceinline__ void rx_pair(const RxParams& p, int64_t q, float2& a, float2& b) {
+    if (q >= 0 && q + 1 < p.N && p.x_aligned16) {
+        InIO<InT>::load_pair(p.x, q, a, b);
+    } else {
+        a = rx_sample<InT>(p, q);
+        b = rx_sample<InT>(p, q + 1);
+    }
+}
+
+// carrier.next() + pll.phase_offset (demodulator.rs:50): one f32 add, exact for offset 0
+__device__ __forceinline__ float rx_phase(const RxParams& p, float carrier) {
+#pragma clang fp contract(off)
+    return carrier + p.phase_offset;
+}
+
+// sin / cos of carrier.next() + pll.phase_offset (demodulator.rs:50) on the hardware
+// v_sin/v_cos (argument in turns): turns = fma(carrier, 1/2pi, offset/2pi), the same
+// expression in every RX path (fast, general, VALU), so that results never depend on which
+// path a sample took. For offset 0 it is fl(carrier / 2pi) exactly as __sinf/__cosf take it.
+__device__ __forceinline__ void rx_sincos(const RxParams& p, float carrier, float& s, float& c) {
+    const float rev = __builtin_fmaf(carrier, kRcp2Pi, p.phase_offset * kRcp2Pi);
+    s = __builtin_amdgcn_sinf(rev);
+    c = __builtin_amdgcn_cosf(rev);
+}
+
+// x * e^{-j phase} (or the reference's x.re * (cos, -sin), demodulator.rs:46,53-54) for
+// stream index n = nb + off (nb wave-uniform).
+template <int MIX>
+__device__ __forceinline__ float2 rx_mix(const RxParams& p, int64_t nb, int off, float2 x) {
+    if (nb + off < 0) return make_float2(0.f, 0.f);   // before the stream: zero history
+    float s, c;
+    rx_sincos(p, carrier_phase_off(p.w, p.c0 + (uint64_t)nb, off, p.exact_idx), s, c);
+    if (MIX == MIX_REFERENCE_REAL) return make_float2(x.x * c, x.x * -s);
+    return make_float2(__builtin_fmaf(x.y, s, x.x * c), __builtin_fmaf(-x.x, s, x.y * c));
+}
+
+// Nearest LUT entry, lowest index on ties (squared distance, no contraction).
+__device__ __forceinline__ uint8_t rx_slice_nearest(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    cfloat* lut = (cfloat*)p.slut;
+    const int n = 1 << p.bps;
+    uint32_t best = 0;
+    float bd = __builtin_inff();
+    for (int k = 0; k < n; ++k) {
+        const float dr = re - lut[2 * k], di = im - lut[2 * k + 1];
+        const float d = dr * dr + di * di;
+        if (d < bd) { bd = d; best = (uint32_t)k; }
+    }
+    return (uint8_t)best;
+}
+
+// The same for a 4-entry LUT (QPSK), unrolled: the table stays in scalar registers across
+// the tile loop instead of being re-read per decision.
+__device__ __forceinline__ uint8_t rx_slice_nearest4(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    cfloat* lut = (cfloat*)p.slut;
+    uint32_t best = 0;
+    float bd = __builtin_inff();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float dr = re - lut[2 * k], di = im - lut[2 * k + 1];
+        const float d = dr * dr + di * di;
+        if (d < bd) { bd = d; best = (uint32_t)k; }
+    }
+    return (uint8_t)best;
+}
+
+__device__ __forceinline__ uint8_t rx_slice(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    if (p.slicer_kind == SLICER_QAM_AXIS) {
+        const int ms = (int)p.max_symbol;
+        const float fi = (re * p.inv_scale + p.max_symbol) * 0.5f;
+        const float fq = (im * p.inv_scale + p.max_symbol) * 0.5f;
+        const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fi), 0.f), p.max_symbol);
+        const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(fq), 0.f), p.max_symbol);
+        (void)ms;
+        return (uint8_t)((si << p.bits_per_carrier) | sq);
+    }
+    return rx_slice_nearest(p, re, im);
+}
+
+template <typename OutT>
+__device__ __forceinline__ void rx_emit(const RxParams& p, int64_t o, float re, float im) {
+    if (p.out_iq) OutIO<OutT>::store_one(p.out_iq, o, re, im);
+    if (p.out_sym && p.slicer_kind != SLICER_NONE) p.out_sym[o] = rx_slice(p, re, im);
+}
+
+template <typename InT>
+__device__ inline void rx_state_update(const RxParams& p) {
+    for (int i = threadIdx.x; i < p.HL; i += blockDim.x) {
+        const int64_t q = p.N - p.HL + i;
+        if (q >= 0) InIO<InT>::copy(p.hist_new, i, p.x, q);
+        else InIO<InT>::copy(p.hist_new, i, p.hist, q + p.HL);
+    }
+}
+
+// ----------------------------------------------------------------------- RX on MFMA ----
+// Matched filter at the kept instants on the matrix cores (v_mfma_f32_16x16x32_f16):
+//   rows i = 16 groups of 16 consecutive kept instants, cols c = instant in the group,
+//   k = w = offset in a W = 32*NKS sample window ending at the group's last instant,
+//   A[i][w] = z[start_i + w] (mixed input), B[w][c] = h[W - 1 - w - (15 - c)*DEC].
+// Every real operand is split in two f16 halves, a = a_hi + a_lo (round to nearest), and
+//   A*B ~= A_hi*B_hi + A_hi*B_lo + A_lo*B_hi      (dropped A_lo*B_lo < 2^-22 |a||b|)
+// accumulates in f32: 6 MFMAs (re and im rails) per 32-sample k-step, 16x the MAC rate of
+// the f32 MFMA. Range: the taps are scaled by 2^kb on the host (0 when their max is in
+// [2^-3, 2^15)); the mixed samples of a tile by 2^ka, ka = tile_ka of the tile's max |z| (0
+// inside [2^-3, 2^15), so results never depend on how a stream is cut into calls). Outputs
+// are scaled back with ldexp (exact).
+// LDS: four f16 planes (re_hi, re_lo, im_hi, im_lo) and NC shifted copies of the hi/lo
+// reversed-tap table, so that every lane's 8-tap B read is one aligned ds_read_b128.
+
+// Plane position of staged sample e: 16 pad halves after every RW samples. With the row pitch
+// RW + 16 (= 2 mod 4 in 16-B units), the 16 lanes of each ds_read_b128 lane group (rows i at
+// k-offset g, rows i' at g + 1) hit distinct bank quads; a pitch of RW + 8 was 2-way conflicted.
+__host__ __device__ constexpr int rxh_pos(int e, int RW) { return e + 16 * (e / RW); }
+
+// What the steady-state epilogue writes: baseband IQ, QAM-axis decisions, or both
+// (RXE_GEN: any other combination, guarded per store).
+enum { RXE_GEN = 0, RXE_IQ = 1, RXE_SYM = 2, RXE_IQSYM = 3, RXE_NEAREST = 4 };   // | NEAREST: LUT slicer
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// hi = rn_f16(v), lo = rn_f16(v - hi) for two values: one v_cvt_pk_f16_f32 and two
+// v_fma_mix{lo,hi}_f16 that round the exact f32 remainder v - hi straight into the packed
+// lo halves (3 VALU per pair).
+__device__ __forceinline__ void split2(cf2 v, h2& hi, h2& lo) {
+    hi = __builtin_convertvector(v, h2);
+    uint32_t l;
+    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=&v"(l) : "v"(hi), "v"(v.x));
+    asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hi), "v"(v.y));
+    lo = __builtin_bit_cast(h2, l);
+}
+
+// Conjugate mix of one sample, packed: (re, im) = (x*cs + y*sn, y*cs - x*sn) with the same
+// roundings as fma(y, sn, x*cs) / fma(-x, sn, y*cs). cssn = (cs, sn).
+__device__ __forceinline__ cf2 cmix(cf2 x, cf2 cssn) {
+    const cf2 t = x * cssn.xx;
+    return __builtin_elementwise_fma(x.yx, (cf2){cssn.y, -cssn.y}, t);
+}
+
+// Four consecutive input samples (one lane's staging quad).
+template <typename InT> struct Quad;
+template <> struct Quad<float> {
+    struct T { float4 a, b; };
+    __device__ static void split(const T& t, float2 (&x)[4]) {
+        x[0] = make_float2(t.a.x, t.a.y); x[1] = make_float2(t.a.z, t.a.w);
+        x[2] = make_float2(t.b.x, t.b.y); x[3] = make_float2(t.b.z, t.b.w);
+    }
+};
+template <> struct Quad<__half> {
+    using T = uint4;
+    __device__ static void split(const T& t, float2 (&x)[4]) {
+        x[0] = __half22float2(*reinterpret_cast<const __half2*>(&t.x));
+        x[1] = __half22float2(*reinterpret_cast<const __half2*>(&t.y));
+        x[2] = __half22float2(*reinterpret_cast<const __half2*>(&t.z));
+        x[3] = __half22float2(*reinterpret_cast<const __half2*>(&t.w));
+    }
+};
+
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = __builtin_fmaxf(m, __shfl_xor(m, off));
+    return m;
+}
+
+// A tile's scale exponent ka as a function of the biased f32 exponent `ex` of its max |z|
+// (the split-f16 window): 0 when the max lies in [2^-3, 2^15) (or is zero / subnormal /
+// non-finite); otherwise the multiple of 8 that moves it into [2^-3, 2^5) (small tiles) or
+// [2^7, 2^15) (large ones). A pure function of the tile's content, so the fast path (which
+// stages with a predicted ka and keeps the tile only if the prediction equals this) and the
+// general path give identical results; steps of 8 binades keep the prediction from the
+// previous tile right for any slowly varying amplitude.
+__device__ __forceinline__ int tile_ka(int ex) {
+    if (ex <= 0 || ex >= 0xff || (ex >= 127 - 3 && ex < 127 + 15)) return 0;
+    const int k = ex < 127 - 3 ? 8 * ((127 - 3 - ex + 7) / 8) : -8 * ((ex - (127 + 14) + 7) / 8);
+    return k > 120 ? 120 : k;                                // 2^k stays a normal f32
+}
+__device__ __forceinline__ int f32_exp(float m) { return (int)((__float_as_uint(m) >> 23) & 0xff); }
+
+// The tiles one workgroup runs, in order: first, first + step, ... (count of them), of the
+// call's ntiles.
+struct TileSeq { int64_t first, step, count, ntiles; };
+
+// Buffer descriptor over `bytes` bytes at `base` (wave-uniform inputs made provably uniform).
+// Accesses past `bytes` load zeros / are dropped without touching memory.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// clamp(v, 0, cap) of a wave-uniform 64-bit value with 32-bit scalar ops on its halves (a
+// 64-bit compare would go through the vector unit: v_cmp_*_i64 from SGPR pairs).
+__device__ __forceinline__ uint32_t clamp64_u32(int64_t v, uint32_t cap) {
+    const int32_t hi = (int32_t)((uint64_t)v >> 32);
+    const uint32_t lo = (uint32_t)(uint64_t)v;
+    return hi < 0 ? 0u : hi > 0 ? cap : (lo < cap ? lo : cap);
+}
+
+// QAM-axis decisions for (re, im) at once (rx_slice's roundings, contract off), the scale and
+// offset on the packed pipe.
+__device__ __forceinline__ uint8_t rx_slice_qam2(const RxParams& p, float re, float im) {
+#pragma clang fp contract(off)
+    const cf2 f = ((cf2){re, im} * p.inv_scale + p.max_symbol) * 0.5f;
+    const float ms = p.max_symbol;
+    const int si = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(f.x), 0.f), ms);
+    const int sq = (int)__builtin_fminf(__builtin_fmaxf(__builtin_rintf(f.y), 0.f), ms);
+    return (uint8_t)((si << p.bits_per_carrier) | sq);
+}
+
+// One workgroup of 4 waves per tile of TS = 1024 kept instants (persistent: XCD-matched
+// top-down rounds of tiles). Per tile the waves mix, scale and split the tile's input into the
+// LDS planes, reloading every staging slot with the next tile's samples as soon as it is
+// consumed (those loads are in flight through the rest of the staging, the matched filter
+// and the stores), then run the matched filter (16 rows of 16 instants per wave) and store
+// the outputs. Per staged sample the VALU does: the carrier index as one exact f32 add
+// (idx_split), the bit-exact phase (phase_from_f2), the turns and v_sin/v_cos, the packed
+// conjugate mix, an optional exact power-of-two scale, one v_max3 and the split.
+//
+// The f16 range: a tile is staged with a predicted tile_ka (the previous tile's; a call's
+// first from where the previous call ended, a stream's first from its raw input) and each
+// wave votes with three ballots whether the tile's max lies in that exponent's window. A tile
+// outside it, and the call's first tile (its window reads the history), take the general
+// path: per-sample loads, two passes, the same tile_ka -> identical results either way.
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF_ = 4>
+struct RxMfma {
+    using Q = Quad<InT>;
+    using QT = typename Q::T;
+    static constexpr int NT = 256;                              // 4 waves stage every tile
+    static constexpr int NW = NT / 64;
+    static constexpr int NWF = NWF_;                            // of which NWF filter it: 4, or 1 (small calls)
+    static constexpr int TS = NWF * 256;                        // kept instants per tile
+    static constexpr int RW = 16 * DEC;                         // samples per A row
+    static constexpr int W = 32 * NKS;
+    static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
+    static constexpr int NQ = (NS + 3) / 4;                     // quads
+    static constexpr int U = (NQ + NT - 1) / NT;                // quads per lane
+    // Plane layout. decim 4: unpadded, 16-B chunks XOR-swizzled within each aligned group of
+    // 8 chunks — conflict-free A reads (tests/test_lds_banks.py) and 4 KiB less LDS per
+    // workgroup than padding, which lets 4 workgroups share a CU. Otherwise rxh_pos.
+    static constexpr bool SWZ = DEC == 4 && NT == 256;
+    __host__ __device__ static constexpr int ppos(int e) {
+        return SWZ ? ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7)) : rxh_pos(e, RW);
+    }
+    static constexpr int PL = SWZ ? (4 * NQ + 63) & ~63 : (rxh_pos(4 * NQ - 1, RW) + 1 + 7) & ~7;   // halves per plane
+    static constexpr int NC = rx_mfma_table_copies(DEC);
+    static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
+    static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 8 * 4;   // + votes, maxima
+    static constexpr int K_TAB8 = NC * 2 * TB / 8;              // 16-B chunks of the tap tables
+    static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
+    // Waves per SIMD the registers are held to: 4 where the LDS lets 4 workgroups share a CU
+    // (the matched filter then single-buffers its operands to fit 128 VGPRs), else the
+    // compiler's choice.
+    static constexpr int WPE = SWZ && LDS_BYTES <= 40960 ? 4 : 1;
+    static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
+    // plane offset between staging slots (the swizzle repeats every 1024 samples)
+    static constexpr int SLOT_POS = SWZ ? 4 * NT : 4 * NT + 16 * (4 * NT / RW);
+
+    // Rows hold 16 instants aligned to the absolute instant index (k % 16 == column), so an
+    // instant's taps always fall at the same k positions of the 32-wide MFMA sums and the
+    // result never depends on where a call starts. Tile t covers instants
+    // k_first - lead + t*TS ..; outputs before k_first are computed and dropped.
+    __device__ static int lead(const RxParams& p) { return (int)(p.k_first & 15); }
+    __device__ static int64_t q_lo_of(const RxParams& p, int64_t t) {
+        return (p.k_first - lead(p) + t * TS) * DEC + p.D + 15 * DEC - W + 1 - p.n_start;
+    }
+
+    // threadIdx.x as a value the compiler cannot hoist: every lane-dependent quantity is then
+    // computed where it is used instead of once at the kernel entry, where kept live across
+    // the tile loop it would spill (a kernel with scratch runs fewer waves per CU: 38 vs
+    // 32.6 us on C3)
+    __device__ static int tid_() {
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        return t;
+    }
+
+    // Carrier index n_base + e as f32 for the staged samples e of a tile: n_base = A + b with A
+    // a multiple of 2^s exactly representable in f32 (s from the tile's largest index) and b
+    // < 2^22, so fl(A + (b + e)) — one f32 add of two exact values — is the correctly rounded
+    // `n as f32` (needs every index < 2^46: RxParams::idx46, checked on the host).
+    struct Idx { float a, bl; };
+    __device__ static Idx idx_split(uint64_t n_base) {
+        const uint64_t n_max = n_base + NS;
+        const int e = 63 - __builtin_clzll(n_max | 1);
+        const int sh = e > 23 ? e - 23 : 0;
+        const uint64_t A = n_base & ~((1ull << sh) - 1);
+        const float af = __builtin_ldexpf((float)(uint32_t)(A >> sh), sh);      // exact
+        const uint32_t b = (uint32_t)(n_base - A) + 4u * (uint32_t)tid_();
+        return Idx{__builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(uint32_t, af))),
+                   (float)b};
+    }
+
+    // Window of a tile staged with exponent k (see tile_ka): [lo, hi) for its max |z|.
+    __device__ static cf2 window(int k) {
+        return k == 0 ? (cf2){0x1p-3f, 0x1p15f} : k > 0 ? (cf2){0x1p-3f, 0x1p5f} : (cf2){0x1p7f, 0x1p15f};
+    }
+    // After the barrier: do the waves' votes put the staged tile inside the window of k?
+    // (k == 0 also accepts an all-zero / subnormal tile, whose tile_ka is 0.)
+    __device__ static bool fast_ok(const int* votes, int k) {
+        int f = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) f |= votes[w];
+        const bool good = k == 0 ? !(f & 2) && ((f & 1) || !(f & 4)) : (f & 1) && !(f & 2);
+        return __builtin_amdgcn_readfirstlane((int)good) != 0;
+    }
+    __device__ static int read_ka(const float* r) {
+        float m = r[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) m = __builtin_fmaxf(m, r[w]);
+        return __builtin_amdgcn_readfirstlane(tile_ka(f32_exp(m)));
+    }
+
+    // Staging slot u of a tile through a buffer descriptor whose base is the tile window's
+    // first sample and whose size is what of its 4 * NQ samples lies in the chunk (0 bytes: no
+    // next tile). Loads past the size return zeros without touching memory (the spare lanes of
+    // the last slot; a call's last tile; a workgroup's last tile), so the reload of every slot
+    // is unconditional.
+    __device__ static __amdgpu_buffer_rsrc_t window_rsrc(const RxParams& p, int64_t q_lo, bool live) {
+        constexpr int S = sizeof(InT) * 2;
+        const uint32_t w = clamp64_u32(p.N - q_lo, (uint32_t)(4 * NQ));
+        return buf_rsrc(reinterpret_cast<const char*>(p.x) + q_lo * S, live ? w * (uint32_t)S : 0u);
+    }
+    __device__ static QT load_slot(__amdgpu_buffer_rsrc_t r, int voff, int u) {
+        constexpr int S = sizeof(InT) * 2;
+        const int o = voff + 4 * NT * u * S;
+#ifdef MODEM_RX_ABLATE_LOAD          // profiling builds only: no sample loads
+        if constexpr (std::is_same<InT, float>::value) {
+            const float v = 0.5f + 0x1p-20f * (float)(o & 1023);
+            return QT{make_float4(v, -v, v, v), make_float4(-v, v, v, -v)};
+        }
+#endif
+        if constexpr (std::is_same<InT, float>::value) {
+            const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+            const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, 0));
+            return QT{make_float4(a[0], a[1], a[2], a[3]), make_float4(b[0], b[1], b[2], b[3])};
+        } else {
+            return __builtin_bit_cast(QT, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+        }
+    }
+
+    // One 16x16 output block per wave: rows 16 wave .. 16 wave + 15 of the tile. Lane
+    // (i = lane & 15, g = lane >> 4) reads A row i, samples 32s + 8g .. +7, and
+    // B[32s + 8g + j][c = i] = T[32s + 8g + j + (15 - c)*DEC] from the table copy that makes
+    // the read aligned. WPE 4: one k-step's operands at a time (fewer registers; the other
+    // waves hide the LDS latency); otherwise the next k-step's load during this one's MFMAs.
+    __device__ static void fir(const _Float16* pl, const _Float16* tbl, f32x4& dre, f32x4& dim) {
+        constexpr bool DB = WPE < 4;
+        const int lane = tid_() & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const int i = lane & 15, g = lane >> 4;
+        const int ae = (16 * wave + i) * RW + 8 * g;
+        const int xb = 8 * g + (15 - i) * DEC;
+        const int q = xb & 7;
+        const _Float16* brow = tbl + (q / (8 / NC)) * 2 * TB + (xb - q);
+        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;
+        h8 a[2][4], b[2][2];
+        auto load = [&](int s, int c) {
+            const _Float16* ap = pl + ppos(ae + 32 * s);
+            a[c][0] = *reinterpret_cast<const h8*>(ap);
+            a[c][1] = *reinterpret_cast<const h8*>(ap + PL);
+            a[c][2] = *reinterpret_cast<const h8*>(ap + 2 * PL);
+            a[c][3] = *reinterpret_cast<const h8*>(ap + 3 * PL);
+            b[c][0] = *reinterpret_cast<const h8*>(brow + 32 * s);
+            b[c][1] = *reinterpret_cast<const h8*>(brow + TB + 32 * s);
+        };
+        if (DB) load(0, 0);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const int c = DB ? s & 1 : 0;
+            if (!DB) load(s, 0);
+            else if (s + 1 < NKS) load(s + 1, c ^ 1);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][0], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][1], m0, 0, 0, 0);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], b[c][0], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], b[c][0], m0, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        dre = r0;
+        dim = m0;
+    }
+
+    // Split z (4 samples) and write it at plane offset o.
+    __device__ static void put4(_Float16* pl, int o, const float (&zr)[4], const float (&zi)[4]) {
+        h2 rh0, rl0, rh1, rl1, ih0, il0, ih1, il1;
+        split2((cf2){zr[0], zr[1]}, rh0, rl0);
+        split2((cf2){zr[2], zr[3]}, rh1, rl1);
+        split2((cf2){zi[0], zi[1]}, ih0, il0);
+        split2((cf2){zi[2], zi[3]}, ih1, il1);
+        *reinterpret_cast<h4*>(pl + o) = (h4){rh0.x, rh0.y, rh1.x, rh1.y};
+        *reinterpret_cast<h4*>(pl + PL + o) = (h4){rl0.x, rl0.y, rl1.x, rl1.y};
+        *reinterpret_cast<h4*>(pl + 2 * PL + o) = (h4){ih0.x, ih0.y, ih1.x, ih1.y};
+        *reinterpret_cast<h4*>(pl + 3 * PL + o) = (h4){il0.x, il0.y, il1.x, il1.y};
+    }
+
+    // Fast-path staging of one tile from the prefetched registers `pre` at scale 2^k (SC:
+    // k != 0; sc = 2^k, win = window(k)), reloading each slot with the next tile's samples
+    // (`nxt`). Each wave writes its three votes (max >= window lo, >= window hi, normal).
+    template <bool SC>
+    __device__ static void stage(const RxParams& p, _Float16* pl, int* vote, Idx ix, float sc, cf2 win,
+                                 QT (&pre)[U], __amdgpu_buffer_rsrc_t nxt) {
+        const int tid = tid_();
+        int pos0 = ppos(4 * tid);
+        int voff = 4 * tid * (int)sizeof(InT) * 2;
+        float bl = ix.bl;
+        asm volatile("" : "+v"(pos0), "+v"(voff), "+v"(bl));
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const float roff = p.phase_offset * kRcp2Pi;          // rx_sincos: carrier + PLL offset, in turns
+        float mx = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) {   // partial last slot: not this wave's
+                pre[u] = load_slot(nxt, voff, u);
+                continue;
+            }
+            float2 x[4];
+            Q::split(pre[u], x);
+            const int e0 = 4 * (tid + NT * u);
+            const float bu = bl + (float)(4 * NT * u);
+            const cf4 nf = (bu + (cf4){0.f, 1.f, 2.f, 3.f}) + ix.a;   // exact, then one rounding
+            const cf4 rv = __builtin_elementwise_fma(phase_from_f4(p.w, nf), (cf4){kRcp2Pi, kRcp2Pi, kRcp2Pi, kRcp2Pi},
+                                                     (cf4){roff, roff, roff, roff});
+            const float sn[4] = {__builtin_amdgcn_sinf(rv.x), __builtin_amdgcn_sinf(rv.y),
+                                 __builtin_amdgcn_sinf(rv.z), __builtin_amdgcn_sinf(rv.w)};
+            const float cs[4] = {__builtin_amdgcn_cosf(rv.x), __builtin_amdgcn_cosf(rv.y),
+                                 __builtin_amdgcn_cosf(rv.z), __builtin_amdgcn_cosf(rv.w)};
+            float zr[4], zi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                cf2 z = MIX == MIX_REFERENCE_REAL ? (cf2){x[j].x * cs[j], x[j].x * -sn[j]}
+                                                  : cmix((cf2){x[j].x, x[j].y}, (cf2){cs[j], sn[j]});
+                if (SC) z = z * sc;
+                zr[j] = z.x;
+                zi[j] = z.y;
+                // only the last slot can reach past the tile: its extra samples are not counted
+                if ((u + 1) * 4 * NT <= NS || e0 + j < NS)
+                    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j]), "v"(zi[j]));
+            }
+            if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, pos0 + u * SLOT_POS, zr, zi);
+            // (not hoisted above the mix: the slot's registers would be copied out first)
+            __builtin_amdgcn_sched_barrier(0);
+            pre[u] = load_slot(nxt, voff, u);                  // the next tile's slot u, same registers
+            __builtin_amdgcn_sched_barrier(0);                 // one quad's temporaries at a time
+        }
+        // three votes per wave instead of a max reduction
+        const bool blo = __ballot(mx >= win.x) != 0, bhi = __ballot(mx >= win.y) != 0,
+                   bn = __ballot(mx >= 0x1p-126f) != 0;
+        if ((tid & 63) == 0) vote[wave] = (blo ? 1 : 0) | (bhi ? 2 : 0) | (bn ? 4 : 0);
+    }
+
+    // D[row][col]: row = 4*(lane>>4) + r, col = lane&15 -> instant ot + 16*row + col. Stores
+    // through buffer descriptors over the wave's instants that are in the call: those before
+    // the call's first (ot < 0: a lane offset below the base wraps out of range) and past its
+    // last are dropped without a branch.
+    template <int EM>
+    __device__ static void emit(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
+        const int lane = tid_() & 63;
+        if (EM == RXE_GEN) {                   // any other output combination: guarded stores
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t o = ot + 16 * (4 * (lane >> 4) + r) + (lane & 15);
+                if (o >= 0 && o < p.nout)
+                    rx_emit<OutT>(p, o, GAIN * __builtin_ldexpf(dre[r], -kab), GAIN * __builtin_ldexpf(dim[r], -kab));
+            }
+            return;
+        }
+        const bool neg = (int32_t)((uint64_t)ot >> 32) < 0;   // before the call's first instant
+        const int64_t ob = neg ? 0 : ot;
+        const int sh = neg ? (int)ot : 0;                    // -15 .. 0
+        const uint32_t nk = clamp64_u32(p.nout - ob, 256u);
+        const __amdgpu_buffer_rsrc_t riq = buf_rsrc(reinterpret_cast<OutT*>(p.out_iq) + 2 * ob, nk * 2 * sizeof(OutT));
+        const __amdgpu_buffer_rsrc_t rsy = buf_rsrc(p.out_sym + ob, nk);
+        f32x4 re = dre, im = dim;
+        if (kab != 0) {                        // uniform
+#pragma unroll
+            for (int r = 0; r < 4; ++r) { re[r] = __builtin_ldexpf(re[r], -kab); im[r] = __builtin_ldexpf(im[r], -kab); }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t off = (uint32_t)(16 * (4 * (lane >> 4) + r) + (lane & 15) + sh);
+            const float a = re[r] * GAIN, b = im[r] * GAIN;
+            if (EM & RXE_IQ) {
+                if constexpr (std::is_same<OutT, float>::value)
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(a, b)), riq, 8 * off, 0, 0);
+                else
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, __floats2half2_rn(a, b)), riq, 4 * off, 0, 0);
+            }
+            if (EM & RXE_SYM) {
+                const uint8_t sy = !(EM & RXE_NEAREST) ? rx_slice_qam2(p, a, b)
+                                 : p.bps == 2 ? rx_slice_nearest4(p, a, b) : rx_slice_nearest(p, a, b);
+                __builtin_amdgcn_raw_buffer_store_b8(sy, rsy, off, 0, 0);
+            }
+        }
+    }
+
+    // General path for tile t (all waves): two passes over its samples (max, then tile_ka
+    // scale + split), the matched filter, the outputs in range. Returns its tile_ka.
+    template <int EM>
+    __device__ __forceinline__ static int slow_tile(const RxParams& p, _Float16* pl, const _Float16* tbl, float* reds, int64_t t,
+                                    int kb, int ld) {
+        // lane values recomputed here, not hoisted to the kernel entry (where, live across
+        // the tile loop, they would spill)
+        const int tid = tid_();
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int64_t q_lo = q_lo_of(p, t), n_lo = q_lo + p.n_start;
+        // 1. The window's raw samples into the planes' LDS (free until this tile is staged),
+        //    through a buffer descriptor over the chunk (out of range loads return zeros without
+        //    a memory access, so they carry no branches), issued in batches of 8 per lane with
+        //    the LDS writes after each batch: the compiler otherwise waited for every load pair
+        //    before issuing the next (vmcnt(0) per sample), 17 round trips on C3 — the call's
+        //    first tile took 10-16 us against ~3.5 for a fast one (r03 stamps, tools/stamps.py).
+        //    The window's samples before the chunk (only a call's first tile has them) are then
+        //    patched in from the history.
+        float2* raw = reinterpret_cast<float2*>(pl);
+        {
+            constexpr int S = sizeof(InT) * 2;
+            constexpr int NK = (NS + NT - 1) / NT, BATCH = 8;
+            const int64_t ex = q_lo >= 0 ? 0 : -q_lo;                 // first window sample in the chunk
+            const int64_t qx = q_lo + ex;
+            const int64_t nx = p.N - qx < NS ? p.N - qx : NS;
+            const __amdgpu_buffer_rsrc_t rx = buf_rsrc(reinterpret_cast<const char*>(p.x) + qx * S,
+                                                       (uint32_t)(nx > 0 ? nx : 0) * S);
+            const int ox = (int)ex;
+            auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+                if constexpr (std::is_same<InT, float>::value)
+                    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+                else
+                    return __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0)));
+            };
+#pragma unroll
+            for (int k0 = 0; k0 < NK; k0 += BATCH) {
+                float2 v[BATCH];
+#pragma unroll
+                for (int b = 0; b < BATCH; ++b)       // < 0: wraps, out of range -> 0
+                    if (k0 + b < NK) v[b] = ld(rx, (uint32_t)(tid + (k0 + b) * NT - ox) * S);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int b = 0; b < BATCH; ++b) {
+                    const int e = tid + (k0 + b) * NT;
+                    if (k0 + b < NK && ((k0 + b + 1) * NT <= NS || e < NS)) raw[e] = v[b];
+                }
+            }
+            if (ox > 0) {                                             // uniform: the call's first tile
+                const int64_t hb = q_lo + p.HL;                       // history index of sample 0
+                const int64_t eh = hb >= 0 ? 0 : -hb;                 // first window sample in the history
+                const int64_t nhist = p.HL - (hb + eh);
+                const __amdgpu_buffer_rsrc_t rh = buf_rsrc(reinterpret_cast<const char*>(p.hist) + (hb + eh) * S,
+                                                           (uint32_t)(nhist > 0 ? nhist : 0) * S);
+                const int oh = (int)eh;
+                for (int k = 0; k * NT < ox && k < NK; ++k) {         // uniform bounds
+                    const int e = tid + k * NT;
+                    const float2 w = ld(rh, (uint32_t)(e - oh) * S);
+                    if (e < ox && e < NS) raw[e] = w;
+                }
+            }
+        }
+        __syncthreads();
+        // 2. Mix (rx_mix: the same values as the fast path's), the tile's max.
+        float zr[U][4], zi[U][4];
+        float mx = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e0 = 4 * (tid + NT * u);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float2 z = make_float2(0.f, 0.f);
+                if (e0 + j < NS) z = rx_mix<MIX>(p, n_lo, e0 + j, raw[e0 + j]);
+                zr[u][j] = z.x;
+                zi[u][j] = z.y;
+                mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(z.x), __builtin_fabsf(z.y)));
+            }
+        }
+        mx = wave_max(mx);
+        if ((tid & 63) == 0) reds[wave] = mx;
+        __syncthreads();                       // also: every raw read done before the planes overwrite it
+        // 3. Scale by 2^tile_ka, split, stage.
+        const int ka = read_ka(reds);
+        const float sc = __builtin_ldexpf(1.0f, ka);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e0 = 4 * (tid + NT * u);
+            if (e0 >= NS) continue;
+            float a[4], b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { a[j] = zr[u][j] * sc; b[j] = zi[u][j] * sc; }
+            put4(pl, ppos(e0), a, b);
+        }
+        __syncthreads();
+        f32x4 dre, dim;
+        if (wave < NWF) {                      // uniform
+            fir(pl, tbl, dre, dim);
+            emit<EM>(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
+        }
+        __syncthreads();                       // the planes are restaged next
+        return ka;
+    }
+
+    // A tile on the fast path: its window starts inside the chunk and its first instant is
+    // kept (samples past the chunk's end load as zeros and instants past the call's last are
+    // not stored, both through the buffer descriptors' bounds); the call's first tile, which
+    // reads the history, takes the general path. `fast`: 4-B aligned input, carrier indices
+    // < 2^46 (idx_split).
+    struct Ctx {
+        bool fast;
+        int kb, ld;
+    };
+
+    // The workgroup's tiles t_i = first + i * step (i < count, step = -grid: top-down), walked
+    // with running values so that a tile's scalar bookkeeping is a few adds, not 64-bit
+    // multiplies and compares (the RX is issue-bound: 100 extra s_nop per tile cost it ~1.3 us,
+    // profiles/r03_sensitivity.txt): the tile, its window offset q = q_lo_of(t), and the
+    // number of leading tiles on the fast path (q and t only decrease along the walk, so the
+    // tiles with q >= 0 and t * TS >= lead come first).
+    struct Walk {
+        int64_t t, q, step, dq, last;          // tile, q_lo_of(t), steps per tile, the call's last tile
+        int32_t i, count, nfull;               // position, tiles in the walk, leading full tiles
+        __device__ void next() { ++i; t += step; q += dq; }
+        __device__ bool full() const { return i < nfull; }
+        __device__ bool next_full() const { return i + 1 < nfull && i + 1 < count; }
+    };
+    __device__ static Walk walk(const RxParams& p, const TileSeq& sq, bool fast) {
+        Walk w;
+        w.t = sq.first;
+        w.step = sq.step;
+        w.dq = sq.step * (int64_t)(TS * DEC);
+        w.q = q_lo_of(p, sq.first);
+        w.last = sq.ntiles - 1;
+        w.i = 0;
+        w.count = (int32_t)sq.count;
+        w.nfull = 0;
+        if (fast) {                            // the smallest full tile: q_lo_of(t) >= 0, t * TS >= lead
+            const int64_t q0 = q_lo_of(p, 0);
+            int64_t tmin = q0 >= 0 ? 0 : (-q0 + TS * DEC - 1) / (TS * DEC);
+            if (lead(p) > 0 && tmin < 1) tmin = 1;
+            if (sq.first >= tmin) {
+                const int64_t n = (sq.first - tmin) / -sq.step + 1;
+                w.nfull = (int32_t)(n < sq.count ? n : sq.count);
+            }
+        }
+        return w;
+    }
+
+    // Tiles from w.i on while their staging exponent keeps its class (SC: nonzero). Returns
+    // at the end of the walk, or after the barrier of a tile the general path must redo.
+    template <bool SC, int EM>
+    __device__ __forceinline__ static void loop(const RxParams& p, _Float16* pl, const _Float16* tbl, int* votes, Walk& w,
+                                const Ctx& cx, QT (&pre)[U], int kpred) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const float sc = __builtin_ldexpf(1.0f, kpred);
+        const cf2 win = window(kpred);
+#ifdef MODEM_STAMPS
+        const int& i = w.i;
+#endif
+        while (w.i < w.count) {
+            const int64_t t = w.t;
+            const bool fi = w.full();
+            const bool pf = w.next_full();
+            const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? w.q + w.dq : 0, pf);
+            const Idx ix = idx_split(p.c0 + (uint64_t)(w.q + p.n_start));
+            // the staging (VALU-bound, the limiting stage) issues ahead of the other
+            // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
+            // event, +0.8 % bench (profiles/r02_store_layout_ab.txt; priority 3: no better)
+            RX_STAMP(i, 0);
+            __builtin_amdgcn_s_setprio(1);
+            stage<SC>(p, pl, votes, ix, sc, win, pre, nxt);
+#ifdef MODEM_RX_PAD_SNOP            // sensitivity builds only: extra scalar issue per tile
+#pragma unroll
+            for (int k = 0; k < MODEM_RX_PAD_SNOP; ++k) asm volatile("s_nop 0");
+#endif
+#ifdef MODEM_RX_PAD_VALU            // sensitivity builds only: extra vector issue per tile
+            {
+                float dv = (float)threadIdx.x;
+#pragma unroll
+                for (int k = 0; k < MODEM_RX_PAD_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(dv));
+                asm volatile("" :: "v"(dv));
+            }
+#endif
+            __builtin_amdgcn_s_setprio(0);
+            RX_STAMP(i, 1);
+            __syncthreads();
+            RX_STAMP(i, 2);
+            if (!(fi && fast_ok(votes, kpred))) return;
+            if (t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
+            f32x4 dre, dim;
+            if (NWF == NW || wave < NWF) {     // uniform
+#ifdef MODEM_RX_ABLATE_FIR          // profiling builds only: no matched filter
+                dre = (f32x4){1.f, 1.f, 1.f, 1.f}; dim = dre;
+#else
+                fir(pl, tbl, dre, dim);
+#endif
+                RX_STAMP(i, 3);
+#ifdef MODEM_RX_ABLATE_STORE        // profiling builds only: no output stores
+                asm volatile("" :: "v"(dre[0] + dre[1] + dre[2] + dre[3] + dim[0] + dim[1] + dim[2] + dim[3]));
+#else
+                emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
+#endif
+                RX_STAMP(i, 4);
+            }
+            __syncthreads();                   // the planes are restaged next
+            RX_STAMP(i, 5);
+            w.next();
+        }
+    }
+
+    template <int EM>
+    __device__ __forceinline__ static void run(const RxParams& p, _Float16* pl, _Float16* tbl, const _Float16* __restrict__ tables,
+                               float* red, const TileSeq sq, int64_t bid) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        RX_STAMP(7, 0);
+        const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
+        Walk w = walk(p, sq, cx.fast);
+        int* votes = reinterpret_cast<int*>(red);            // [4]
+        float* reds = red + 4;                               // [4]
+        QT pre[U];
+        auto prefetch = [&](int64_t q, bool live) {
+            const __amdgpu_buffer_rsrc_t r = window_rsrc(p, live ? q : 0, live);
+            const int voff = 4 * tid_() * (int)sizeof(InT) * 2;
+#pragma unroll
+            for (int u = 0; u < U; ++u) pre[u] = load_slot(r, voff, u);
+        };
+        // the tap tables into LDS, their loads issued before the first tile's so that the two
+        // memory latencies at the kernel's start overlap (the table stores wait for the table
+        // loads only)
+        constexpr int NTB = K_TAB8 / NT + (K_TAB8 % NT ? 1 : 0);
+        h8 tv[NTB];
+#pragma unroll
+        for (int k = 0; k < NTB; ++k) {
+            const int j = tid_() + k * NT;
+            if (j < K_TAB8) tv[k] = reinterpret_cast<const h8*>(tables)[j];
+        }
+        const bool f0 = w.full();
+        prefetch(w.q, f0);
+#pragma unroll
+        for (int k = 0; k < NTB; ++k) {
+            const int j = tid_() + k * NT;
+            if (j < K_TAB8) reinterpret_cast<h8*>(tbl)[j] = tv[k];
+        }
+        __syncthreads();
+        // the first prediction: where the previous call ended (any exponent tile_ka can give)
+        const int kin = *p.ka_in;
+        int kpred = kin >= -120 && kin <= 120 && (kin & 7) == 0 ? kin : 0;
+        if (f0 && kin == INT32_MIN) {          // a stream's first call: from the first tile's raw input
+            float mx = 0.f;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) continue;
+                float2 x[4];
+                Q::split(pre[u], x);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(x[j].x), "v"(x[j].y));
+            }
+            mx = wave_max(mx);
+            if ((tid_() & 63) == 0) reds[wave] = mx;
+            __syncthreads();
+            kpred = read_ka(reds);
+            __syncthreads();
+        }
+#ifdef MODEM_STAMPS
+        modem_stamp(7, 1, __builtin_amdgcn_s_memrealtime());
+        modem_stamp(7, 2, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
+        modem_stamp(7, 3, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
+        modem_stamp(7, 6, (unsigned long long)sq.first);
+        const int& i = w.i;
+#endif
+        while (w.i < w.count) {
+            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
+            else loop<true, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
+            if (w.i < w.count) {               // tile w.t on the general path (one place in the code)
+                RX_STAMP(i, 6);
+                kpred = slow_tile<EM>(p, pl, tbl, reds, w.t, cx.kb, cx.ld);
+                if (w.t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
+                RX_STAMP(i, 7);
+                w.next();
+                // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
+                // not held across the general path, which has no registers to spare)
+                prefetch(w.q, w.i < w.count && w.full());
+            }
+        }
+        RX_STAMP(7, 4);
+#ifdef MODEM_STAMPS
+        modem_stamp(7, 5, __builtin_amdgcn_s_memrealtime());
+#endif
+    }
+};
+
+// One channel's share of a launch: workgroup `bid` of `nb` working on channel p, with the
+// epilogue EM chosen on the host (rx_mfma_em): each kernel keeps only its own stores.
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
+__device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* __restrict__ tables, int64_t bid,
+                                             int64_t nb) {
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
+    _Float16* pl = lds_h;                                   // 4 sample planes
+    _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
+    float* red = reinterpret_cast<float*>(tbl + K::NC * 2 * K::TB);
+    if (bid == 0) rx_state_update<InT>(p);
+    const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;
+    // Rounds of nb tiles from the top down, tile R - (r + 1) nb + bid in round r. The TX hands
+    // its tiles out grid-strided (tile i to workgroup i mod grid, both grids multiples of 8, so
+    // tile i is written on XCD slot i mod 8); the RX's first round then reads the ~32 MiB the
+    // TX wrote last, each tile on the XCD slot that wrote it (blocks b and b + 8 share an XCD).
+    // C3: 35.0 -> 33.8 us against contiguous ranges per workgroup; the same rounds with the
+    // slots shifted by 1 or 4 measured 38.1-39.1 us (PMC FETCH_SIZE per launch unchanged).
+    if (ntiles <= 0) {                         // no tile: the next call predicts as this one did
+        if (bid == 0 && threadIdx.x == 0) *p.ka_out = *p.ka_in;
+        return;
+    }
+    const int64_t R = (ntiles + nb - 1) / nb * nb;
+    TileSeq sq{R - nb + bid, -nb, R / nb, ntiles};
+    if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }
+    if (sq.count <= 0) return;
+    K::template run<EM>(p, pl, tbl, tables, red, sq, bid);
+}
+
+// The epilogue specialisation for a call: stores known at compile time for the loopback
+// chain's outputs (f32 or f16 I/Q in and out, complex mix), else the guarded general one.
+template <typename InT, int MIX, typename OutT>
+__host__ inline int rx_mfma_em(const RxParams& p) {
+    const bool loop = std::is_same<InT, OutT>::value && MIX == MIX_COMPLEX;
+    if (!loop) return RXE_GEN;
+    const bool qam = p.slicer_kind == SLICER_QAM_AXIS && p.out_sym;
+    if (p.out_iq && qam) return RXE_IQSYM;
+    if (std::is_same<InT, float>::value) {
+        if (p.out_iq && p.out_sym && p.slicer_kind == SLICER_NEAREST) return RXE_IQSYM | RXE_NEAREST;
+        if (p.out_iq && !p.out_sym) return RXE_IQ;
+        if (!p.out_iq && qam) return RXE_SYM;
+    }
+    return RXE_GEN;
+}
+
+// Tile size by the work: 1024-instant tiles (4 filter waves) when the call has at least four
+// per CU, else 256-instant tiles staged by 4 waves and filtered by one, so that a small call
+// (C2: 2^18 instants) still spreads its staging over every SIMD. The filter of a 16-instant
+// row is the same code either way: results do not depend on the choice.
+inline bool rx_small_tiles(int64_t ninst) { return ninst < (int64_t)4 * 1024 * device_cus(); }
+
+}  // namespace mk

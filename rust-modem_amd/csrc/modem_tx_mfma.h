@@ -1,0 +1,499 @@
+// rust-modem_amd/csrc/modem_tx_mfma.h — the TX pulse-shaping FIR on the matrix cores (TxMfma,
+// tx_mfma_body) and the symbol-mapping helpers it shares with the other TX kernels: included
+// by modem_tx.hip (tx_mfma, tx_mfma_batch) and modem_chain.hip (the fused TX->RX period).
+#pragma once
+#include "modem_device.h"
+
+namespace mk {
+
+// Diagnostic builds only (-DMODEM_STAMPS, tools/stamps.py --kernel tx): s_memtime per wave at the
+// phase boundaries of each TX tile (lane 0's vector store into a buffer nothing else reads).
+// Layout [block * 4 + wave][tile slot 0..7][point 0..7]; slot 7: entry / realtime / HW_ID / XCC_ID
+// / exit / realtime.
+#ifdef MODEM_STAMPS
+constexpr int kTxStampWaves = 8192, kTxStampTiles = 8, kTxStampPts = 8;
+static __device__ unsigned long long g_modem_tx_stamps[kTxStampWaves * kTxStampTiles * kTxStampPts];
+__device__ __forceinline__ void modem_tx_stamp(int tile, int pt, unsigned long long v) {
+    const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && w < kTxStampWaves && tile < kTxStampTiles)
+        g_modem_tx_stamps[((size_t)w * kTxStampTiles + tile) * kTxStampPts + pt] = v;
+}
+#define TX_STAMP(t, k) modem_tx_stamp((int)(t), (k), __builtin_amdgcn_s_memtime())
+#else
+#define TX_STAMP(t, k) ((void)0)
+#endif
+
+// ---------------------------------------------------------------- symbol mapping (TX) ----
+// bytes_to_bits (digital/util.rs:5-11) of symbol m's bits, MSB first, `b & 1` per byte.
+__device__ __forceinline__ uint32_t tx_symbol_index(const TxParams& p, int64_t m) {
+    const int bps = p.bps;
+    if (p.fast_bits) {
+        const uint8_t* b = p.bits + m * bps;
+        if (bps == 4) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(b);
+            return ((v & 1u) << 3) | ((v >> 6) & 4u) | ((v >> 15) & 2u) | ((v >> 24) & 1u);
+        }
+        if (bps == 2) {
+            const uint32_t v = *reinterpret_cast<const uint16_t*>(b);
+            return ((v & 1u) << 1) | ((v >> 8) & 1u);
+        }
+        if (bps == 1) return b[0] & 1u;
+        if (bps == 8) {
+            const uint64_t v = *reinterpret_cast<const uint64_t*>(b);
+            uint32_t idx = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) idx |= (uint32_t)((v >> (8 * q)) & 1u) << (7 - q);
+            return idx;
+        }
+    }
+    uint32_t idx = 0;
+    const int64_t l0 = m * bps;
+    for (int q = 0; q < bps; ++q) {
+        const int64_t l = l0 + q;   // logical bit position in [carry | bits]
+        const uint8_t b = l < p.ncarry ? p.carry[l] : p.bits[l - p.ncarry];
+        idx = (idx << 1) | (b & 1u);
+    }
+    return idx;
+}
+
+__device__ __forceinline__ float2 tx_symbol_value(const TxParams& p, int64_t m) {
+    if (m < 0) return m >= -(int64_t)(p.K - 1) ? p.hist[m + p.K - 1] : make_float2(0.f, 0.f);
+    if (m >= p.nsym_valid) return make_float2(0.f, 0.f);
+    return p.lut[tx_symbol_index(p, m)];
+}
+
+// Streaming state for the next call, written by workgroup 0 into the other buffers.
+__device__ inline void tx_state_update(const TxParams& p) {
+    for (int i = threadIdx.x; i < p.K - 1; i += blockDim.x)
+        p.hist_new[i] = tx_symbol_value(p, p.nsym - (p.K - 1) + i);
+    if (p.update_carry) {
+        for (int i = threadIdx.x; i < p.ncarry_new; i += blockDim.x) {
+            const int64_t l = p.nsym * p.bps + i;
+            p.carry_new[i] = l < p.ncarry ? p.carry[l] : p.bits[l - p.ncarry];
+        }
+    }
+}
+
+// bytes_to_bits (digital/util.rs:5-11) of a little-endian word holding bps bytes, branch-free:
+// the LSB of byte i sits at bit 8i; one multiply moves it to bit 27-i (32-bit form) or 63-i
+// (64-bit form) without carries (all partial-product bit positions are distinct).
+__device__ __forceinline__ uint32_t word_index(uint64_t v, int bps) {
+    if (bps <= 4) {
+        const uint32_t b = (uint32_t)v & 0x01010101u;
+        return ((b * 0x08040201u) >> 24) >> (4 - bps);
+    }
+    const uint64_t b = v & 0x0101010101010101ull;
+    return (uint32_t)((b * 0x8040201008040201ull) >> 56) >> (8 - bps);
+}
+
+// ----------------------------------------------------------------------- TX on MFMA ----
+// The zero-stuffed polyphase FIR on the matrix cores (v_mfma_f32_16x16x32_f16):
+//   rows i  = 16 row-blocks of SB = 16/SPS consecutive symbols,
+//   cols j  = (symbol c in the block, phase p) -> sample SPS*c + p of the block (16 samples),
+//   k  = o  = offset in a W = 32*NKS symbol window ending at the block's last symbol,
+//   A[i][o] = a[block_i - PRE + o] (symbol values, from LDS), B[o][j] = h[p + SPS*(c + PRE - o)].
+// As on the RX, every operand is split in two f16 halves (a = a_hi + a_lo, round to nearest)
+// and A*B ~= A_hi*B_hi + A_hi*B_lo + A_lo*B_hi accumulates in f32 (6 MFMAs per k-step for the
+// re and im rails). The LUT and the taps are scaled by exact powers of two on the host
+// (2^lut_scale_exp, 2^tap_scale_exp; 0 when the maxima already lie in [2^-3, 2^15), else into
+// [2^14, 2^15)), split there, and the outputs are scaled back. When every LUT component is an
+// integer multiple of one scale s (QAM, BPSK at pi/4, QPSK at 0, BASK) the symbols are the
+// exact f16 integer levels, s is folded into the taps and the A_lo products vanish. Row-blocks are aligned to the absolute symbol index
+// (lead = symbols before this call, mod SB), so a symbol always meets the same taps at the
+// same k positions and a stream cut into calls gives the same samples as one call.
+// Sample-and-hold (no taps) stays on the exact VALU kernels.
+template <int SPS, int SUB_> struct TxMfmaCfg {
+    static constexpr int SB = 16 / SPS;          // symbols per row-block
+    static constexpr int NT = 256;               // 4 waves
+    static constexpr int SUB = SUB_;             // 16x16 tiles per wave per tile: 4, 1 (small calls)
+    static constexpr int TS = 4 * SUB * 16 * SB; // symbols per workgroup tile
+    static constexpr int NCOP = SB % 4 == 0 ? 1 : 4 / SB;   // plane copies (8-B aligned A reads)
+};
+
+// Carrier mix of one sample, packed: (re, im) = (y*cs - yi*sn, y*sn + yi*cs), y = (yr, yi),
+// cssn = (cs, sn) straight from v_sin/v_cos.
+__device__ __forceinline__ cf2 tx_cmix(cf2 y, cf2 cssn) {
+    // vector ops (v_pk_mul_f32 + v_pk_fma_f32 with op_sel / neg modifiers): visible to the
+    // compiler's hazard recognizer, which pads only where a v_sin/v_cos result is read too early
+    const cf2 t = y * cssn.xx;
+    return __builtin_elementwise_fma(y.yx, (cf2){-cssn.y, cssn.y}, t);
+}
+
+typedef _Float16 th8 __attribute__((ext_vector_type(8)));
+typedef _Float16 th4 __attribute__((ext_vector_type(4)));
+
+template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB_ = 4>
+struct TxMfma {
+    using C = TxMfmaCfg<SPS, SUB_>;
+    static constexpr int SB = C::SB, NT = C::NT, SUB = C::SUB, TS = C::TS, NCOP = C::NCOP;
+    static constexpr int W = 32 * NKS;             // window symbols per row-block
+    static constexpr int PRE = W - SB;             // window symbols before a row-block
+    static constexpr int NE = TS + PRE;            // symbols staged per tile
+    static constexpr int U = (NE + NT - 1) / NT;   // staging slots per lane
+    static constexpr int PLN = (NE + 3 * 4 + 7) & ~7;   // halves per plane copy
+    // LDS: NCOP copies x 4 planes (re_hi, re_lo, im_hi, im_lo) of PLN halves, then the split
+    // LUT (4 halves per entry)
+    // Halves between plane copies. ds_read2_b64 is serviced 16 lanes at a time with bank =
+    // dword mod 32 (MI355X_MICROARCH.md §LDS): with 2 copies (sps 8) the odd rows' copy must
+    // sit 28 halves past a multiple of 64, else every read of a 16-lane group is 2-way
+    // conflicted (8 extra LDS cycles per read; 13 M per C5 launch, PMC SQ_LDS_BANK_CONFLICT);
+    // with 4 copies (sps 16) a residue of 16 halves the conflicts of 0.
+    static constexpr int CRES = SB == 2 ? 28 : SB == 1 ? 16 : 0;
+    static constexpr int CST = 4 * PLN + (NCOP > 1 ? (CRES - (4 * PLN) % 64 + 64) % 64 : 0);
+    static constexpr int PLANES = NCOP * CST;
+
+    // Raw bits word of symbol m, BPS bytes (fast path: aligned, no leftover bits).
+    template <int BPS>
+    __device__ static uint64_t load_word(const uint8_t* bits, int64_t m) {
+        const uint8_t* b = bits + m * BPS;
+        if (BPS == 1) return *b;
+        if (BPS == 2) return *reinterpret_cast<const uint16_t*>(b);
+        if (BPS == 4) return *reinterpret_cast<const uint32_t*>(b);
+        return *reinterpret_cast<const uint64_t*>(b);
+    }
+
+    // Symbol e of the tile (window coordinates) into every plane copy: copy c holds symbol e
+    // at half index e + c*SB, so a row-block starting at blk*SB reads copy ((-blk*SB) mod 4)/SB
+    // 8-B aligned.
+    __device__ static void put(_Float16* pl, int e, th4 v) {
+#pragma unroll
+        for (int c = 0; c < NCOP; ++c) {
+            _Float16* q = pl + c * CST + e + c * SB;
+            q[0] = v[0]; q[PLN] = v[1]; q[2 * PLN] = v[2]; q[3 * PLN] = v[3];
+        }
+    }
+
+    // f32 symbol value -> scaled (2^ka) split halves (re_hi, re_lo, im_hi, im_lo), as the host
+    // splits the LUT (round to nearest both times).
+    __device__ static th4 split_value(const TxParams& p, float2 v) {
+        if (p.levels)      // the exact integer level of a history symbol (lo halves zero)
+            return (th4){(_Float16)__builtin_rintf(v.x * p.level_inv), (_Float16)0.0f,
+                         (_Float16)__builtin_rintf(v.y * p.level_inv), (_Float16)0.0f};
+        const float r = __builtin_ldexpf(v.x, p.lut_scale_exp), i = __builtin_ldexpf(v.y, p.lut_scale_exp);
+        const _Float16 rh = (_Float16)r, ih = (_Float16)i;
+        return (th4){rh, (_Float16)(r - (float)rh), ih, (_Float16)(i - (float)ih)};
+    }
+
+    // General staging: first tile (history), leftover bits, flush, any bps. Every lane's symbol
+    // indices (and history values) are loaded first, all in flight together, then looked up in
+    // the LDS copy of the split LUT (the same halves split_value gives the f32 LUT entry): the
+    // per-symbol form waited for each bits load and then for a global LUT load, ~10 serialized
+    // memory round trips per C3 tile.
+    // (e_lo > 0: only the window's symbols from e_lo on, for the sub-tiles that read no others)
+    __device__ __forceinline__ static void stage_slow(const TxParams& p, _Float16* pl, const th4* lut_s, int64_t ms, int e_lo = 0) {
+        constexpr int NK = (NE + NT - 1) / NT;
+        const int tid = threadIdx.x;
+        uint32_t idx[NK];
+        float2 hv[NK];
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int e = tid + k * NT;
+            const int64_t m = ms + e;
+            idx[k] = 0;
+            hv[k] = make_float2(0.f, 0.f);
+            if (e < NE && e >= e_lo) {
+                if (m < 0) { if (m >= -(int64_t)(p.K - 1)) hv[k] = p.hist[m + p.K - 1]; }
+                else if (m < p.nsym_valid) idx[k] = tx_symbol_index(p, m);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int e = tid + k * NT;
+            const int64_t m = ms + e;
+            if (e < NE && e >= e_lo) put(pl, e, m >= 0 && m < p.nsym_valid ? lut_s[idx[k]] : split_value(p, hv[k]));
+        }
+    }
+
+    // 16x16 sub-tile q of this wave: D = sum over the window of A*B (split products).
+    // LV: integer-level symbols (exact f16, no lo plane): 2 MFMAs per rail and k-step, else 3.
+    template <bool LV>
+    __device__ static void fir(const _Float16* pl, int q, const th8 (&bh)[NKS], const th8 (&bl)[NKS],
+                               f32x4& dre, f32x4& dim) {
+        const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+        const int i = lane & 15, g = lane >> 4;
+        const int blk = (wave * SUB + q) * 16 + i;                  // row-block in the tile
+        const int cp = ((4 - ((blk * SB) & 3)) & 3) / (SB < 4 ? SB : 4);   // copy shifting the row to 8 B
+        // opaque lane offset: every plane / k-step read is this base + a non-negative immediate
+        int aoff = (NCOP > 1 ? cp : 0) * CST + blk * SB + (NCOP > 1 ? cp * SB : 0) + 8 * g;
+        asm volatile("" : "+v"(aoff));
+        const _Float16* ar = pl + aoff;
+        typedef _Float16 tq4 __attribute__((ext_vector_type(4), aligned(8)));
+        auto ld8 = [](const _Float16* a) {                          // 8-B aligned 16-B read
+            const tq4 x = *reinterpret_cast<const tq4*>(a), y = *reinterpret_cast<const tq4*>(a + 4);
+            return (th8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+        };
+#ifdef MODEM_ABLATE_FIR
+        const th8 a0 = ld8(ar);
+        dre = (f32x4){(float)a0[0], 0.f, 0.f, 0.f};
+        dim = (f32x4){(float)bh[0][0], 0.f, 0.f, 0.f};
+        return;
+#endif
+        f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;     // one accumulator per rail
+        th8 a[2][4];
+        auto load = [&](int s, int slot) {
+            a[slot][0] = ld8(ar + 32 * s);
+            if (!LV) a[slot][1] = ld8(ar + PLN + 32 * s);
+            a[slot][2] = ld8(ar + 2 * PLN + 32 * s);
+            if (!LV) a[slot][3] = ld8(ar + 3 * PLN + 32 * s);
+        };
+        load(0, 0);
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            const int c = s & 1;
+            if (s + 1 < NKS) load(s + 1, c ^ 1);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bh[s], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bh[s], m0, 0, 0, 0);
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], bl[s], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], bl[s], m0, 0, 0, 0);
+            if (!LV) {
+                r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], bh[s], r0, 0, 0, 0);
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], bh[s], m0, 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        dre = r0;
+        dim = m0;
+    }
+
+    // Full 16x16 tile, carrier index < 2^53: unconditional stores. jt = call sample index of
+    // the sub-tile's first sample. Per sample: packed unscale (2^-kab), bit-exact phase,
+    // sin/cos, packed mix; stores through a uniform base + 32-bit lane offsets.
+    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
+        const int lane = threadIdx.x & 63;
+        int loff = 64 * (lane >> 4) + (lane & 15);          // sample of row r: loff + 16 r
+        asm volatile("" : "+v"(loff));
+        const double nb = (double)(p.s0 + (uint64_t)jt) + (double)loff;
+        cf2 z[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z[r] = (cf2){dre[r], dim[r]};
+        if (unscale.x != 1.0f) {                            // uniform; scale 1 is the usual case
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[r] *= unscale;
+        }
+#ifndef MODEM_ABLATE_MIX
+        if (OUT_MODE != OUT_IQ_BASEBAND) {
+            // rows (0, 1) and (2, 3) as two packed phase pairs, side by side
+            const cf2 nf0 = (cf2){idx_f32(nb), idx_f32(nb + 16.0)};
+            const cf2 nf1 = (cf2){idx_f32(nb + 32.0), idx_f32(nb + 48.0)};
+            const cf2 ph0 = phase_from_f2(p.w, nf0), ph1 = phase_from_f2(p.w, nf1);
+            cf2 sn0, cs0, sn1, cs1;
+            sincos_phase2(ph0, sn0, cs0);
+            sincos_phase2(ph1, sn1, cs1);
+            z[0] = tx_cmix(z[0], (cf2){cs0.x, sn0.x});
+            z[1] = tx_cmix(z[1], (cf2){cs0.y, sn0.y});
+            z[2] = tx_cmix(z[2], (cf2){cs1.x, sn1.x});
+            z[3] = tx_cmix(z[3], (cf2){cs1.y, sn1.y});
+        }
+#endif
+#ifdef MODEM_ABLATE_STORE
+#pragma unroll
+        for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(z[r]));
+#else
+        // wave-uniform base in SGPRs + 32-bit lane byte offsets (saddr + voffset stores)
+        constexpr int SBYTES = (OUT_MODE == OUT_REAL ? 1 : 2) * (int)sizeof(OutT);
+        const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
+        char* ob = reinterpret_cast<char*>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(oa >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)oa));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            char* q = ob + (uint32_t)((loff + 16 * r) * SBYTES);
+            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(q, 0, z[r].x);
+            else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
+        }
+#endif
+    }
+
+    // Partial tile, samples before the call, or carrier index >= 2^53: guarded, 64-bit
+    // indices; the same arithmetic as emit_full (a sample's bits never depend on the path).
+    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
+        const int lane = threadIdx.x & 63;
+        const int64_t jend = p.nsym * SPS;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int off = 16 * (4 * (lane >> 4) + r) + (lane & 15);
+            if (jt + off < 0 || jt + off >= jend) continue;
+            cf2 z = (cf2){dre[r], dim[r]} * unscale;
+            if (OUT_MODE != OUT_IQ_BASEBAND) {
+                float sn, cs;
+                sincos_phase(carrier_phase_off(p.w, p.s0 + (uint64_t)jt, off, p.exact_idx), sn, cs);
+                z = tx_cmix(z, (cf2){cs, sn});
+            }
+            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, jt + off, z.x);
+            else OutIO<OutT>::store_one(p.out, jt + off, z.x, z.y);
+        }
+    }
+
+    // The last xs 16x16 sub-tiles of tile t alone, on the general path (the fused chain,
+    // modem_chain.hip: the samples just before a workgroup's first tile, which its RX window
+    // reads; the workgroup that owns tile t writes the same values there).
+    __device__ __forceinline__ static void tail(const TxParams& p, _Float16* pl, const th4* lut_s, const th8 (&bh)[NKS],
+                                const th8 (&bl)[NKS], int64_t t, int xs, cf2 unscale) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const int g0 = 4 * SUB - xs;                                // first sub-tile emitted
+        stage_slow(p, pl, lut_s, t * TS - p.lead - PRE, g0 * 16 * SB);
+        __syncthreads();
+        const int64_t j0 = (t * TS - p.lead) * SPS;
+#pragma unroll 1
+        for (int q = 0; q < SUB; ++q) {
+            if (wave * SUB + q < g0) continue;                      // wave-uniform
+            f32x4 dre, dim;
+            if (p.levels) fir<true>(pl, q, bh, bl, dre, dim);
+            else fir<false>(pl, q, bh, bl, dre, dim);
+            emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
+        }
+        __syncthreads();                                            // the planes are restaged next
+    }
+
+    // Tiles t0, t0 + ts, ... below t1 (xs > 0: first the last xs sub-tiles of tile t0 - 1). Tile t holds symbols [t*TS - lead, (t+1)*TS - lead) of the call. BPS > 0: bits aligned,
+    // no leftover bits, carrier index < 2^53 (the steady state); BPS == 0: general path only.
+    template <int BPS>
+    __device__ __forceinline__ static void run(const TxParams& p, _Float16* pl, th4* lut_s, const th8 (&bh)[NKS],
+                               const th8 (&bl)[NKS], int64_t t0, int64_t t1, int64_t ts, int xs = 0) {
+        const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int lead = p.lead;
+        const int kab = p.lut_scale_exp + p.tap_scale_exp;
+        const bool lv = p.levels != 0;
+        const float us = __builtin_ldexpf(1.0f, -kab);             // exact (|kab| < 126)
+        const cf2 unscale = {us, us};
+        const int64_t mlast = p.nsym_valid - 1;
+        // full tile: every staged symbol is data of this call, every sample is emitted
+        auto full = [&](int64_t t) {
+            const int64_t ms = t * TS - lead - PRE;
+            return BPS > 0 && ms >= 0 && ms + NE <= p.nsym_valid && t * TS - lead + TS <= p.nsym;
+        };
+        uint64_t pre[U];
+        auto prefetch = [&](int64_t t) {
+            const int64_t ms = t * TS - lead - PRE;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int64_t m = ms + tid + NT * u;
+                m = m < 0 ? 0 : (m > mlast ? mlast : m);
+                pre[u] = load_word<BPS>(p.bits, m);
+            }
+        };
+        int64_t t = t0;
+        // the first tile's bits are requested before the LUT goes to LDS, so that the two
+        // memory latencies at the kernel's start overlap
+        TX_STAMP(7, 0);
+        bool ready = t < t1 && full(t);
+        if (ready) prefetch(t);
+        const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
+        for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = lut_h[i];
+        __syncthreads();   // LUT visible
+        if (xs > 0 && t0 > 0) tail(p, pl, lut_s, bh, bl, t0 - 1, xs, unscale);
+#ifdef MODEM_STAMPS
+        modem_tx_stamp(7, 1, __builtin_amdgcn_s_memrealtime());
+        modem_tx_stamp(7, 2, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
+        modem_tx_stamp(7, 3, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
+        int si = 0;
+#endif
+        while (t < t1) {
+            if (full(t)) {
+                if (!ready) prefetch(t);
+                ready = false;
+                for (; t < t1 && full(t); t += ts) {
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 0);
+#endif
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int e = tid + NT * u;
+                        if (e < NE) put(pl, e, lut_s[word_index(pre[u], BPS)]);
+                    }
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 1);
+#endif
+                    __syncthreads();
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 2);
+#endif
+                    if (t + ts < t1) prefetch(t + ts);   // next bits fly during the MFMAs
+                    const int64_t j0 = (t * TS - lead) * SPS;
+#pragma unroll
+                    for (int q = 0; q < SUB; ++q) {
+                        f32x4 dre, dim;
+                        if (lv) fir<true>(pl, q, bh, bl, dre, dim);
+                        else fir<false>(pl, q, bh, bl, dre, dim);
+                        // the epilogue (carrier phase, sin/cos, mix, stores) issues ahead
+                        // of the other workgroups' staging and filter: +0.6 % C3 bench in
+                        // three interleaved pairs (profiles/r02_store_layout_ab.txt)
+                        __builtin_amdgcn_s_setprio(1);
+                        emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
+                        __builtin_amdgcn_s_setprio(0);
+                    }
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 4);
+#endif
+                    __syncthreads();                     // the window is restaged next trip
+#ifdef MODEM_STAMPS
+                    TX_STAMP(si, 5);
+                    ++si;
+#endif
+                }
+            } else {
+#ifdef MODEM_STAMPS
+                TX_STAMP(si, 6);
+#endif
+                stage_slow(p, pl, lut_s, t * TS - lead - PRE);
+                __syncthreads();
+                const int64_t j0 = (t * TS - lead) * SPS;
+#pragma unroll 1
+                for (int q = 0; q < SUB; ++q) {
+                    f32x4 dre, dim;
+                    if (lv) fir<true>(pl, q, bh, bl, dre, dim);
+                    else fir<false>(pl, q, bh, bl, dre, dim);
+                    emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
+                }
+                __syncthreads();
+#ifdef MODEM_STAMPS
+                TX_STAMP(si, 7);
+                ++si;
+#endif
+                t += ts;
+            }
+        }
+        TX_STAMP(7, 4);
+#ifdef MODEM_STAMPS
+        modem_tx_stamp(7, 5, __builtin_amdgcn_s_memrealtime());
+#endif
+    }
+};
+
+// One channel's share of a launch: workgroup `bid` of `nb` working on channel p.
+template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
+__device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __restrict__ bfrag,
+                                             int64_t bid, int64_t nb) {
+    using K = TxMfma<SPS, NKS, OUT_MODE, OutT, SUB>;
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds_t[];
+    _Float16* pl = lds_t;
+    th4* lut_s = reinterpret_cast<th4*>(lds_t + K::PLANES);
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (bid == 0) tx_state_update(p);
+    th8 bh[NKS], bl[NKS];                        // this lane's B fragments (hi, lo) per k-step
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        bh[s] = bfrag[(2 * s) * 64 + lane];
+        bl[s] = bfrag[(2 * s + 1) * 64 + lane];
+    }
+    const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
+    // tiles bid, bid + nb, ...: concurrently running workgroups work on neighbouring tiles
+    // (measured 1 % faster on C3 than contiguous ranges per workgroup)
+    const int64_t t0 = bid, t1 = ntiles, ts = nb;
+    if (t0 >= t1) return;
+    if (p.fast_bits && p.exact_idx) {              // one uniform switch: the tile loop is specialised
+        switch (p.bps) {
+        case 1: K::template run<1>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 2: K::template run<2>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 4: K::template run<4>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 8: K::template run<8>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        }
+    }
+    K::template run<0>(p, pl, lut_s, bh, bl, t0, t1, ts);
+}
+
+// Tile size by the work: 4 sub-tiles per wave when the call has at least four such tiles
+// per CU, else one (a small call, C2: 2^18 symbols, then still spreads over every SIMD). The
+// 16x16 sub-tiles are computed alike either way: results do not depend on the choice.
+inline bool tx_small_tiles(int64_t nsym, int sb) { return nsym < (int64_t)4 * 4 * 4 * 16 * sb * device_cus(); }
+
+}  // namespace mk

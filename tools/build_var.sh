@@ -6,11 +6,11 @@ set -e
 name=$1; shift
 cd "$(dirname "$0")/../rust-modem_amd"
 d=build/var/$name; mkdir -p $d
-for f in tx rx misc; do
+for f in tx rx chain misc; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 -DMODEM_DEV_MIN "$@" \
     -c csrc/modem_$f.hip -o $d/$f.o &
 done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -DMODEM_DEV_MIN "$@" -x hip -c csrc/modem_capi.cpp -o $d/c.o &
 wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $d/tx.o $d/rx.o $d/misc.o $d/c.o -o $d/libmodem_hip.so
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $d/tx.o $d/rx.o $d/chain.o $d/misc.o $d/c.o -o $d/libmodem_hip.so
 echo "built $d/libmodem_hip.so"

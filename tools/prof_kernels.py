@@ -15,11 +15,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c3", choices=sorted(bench.WORKLOADS))
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--only", choices=["tx", "rx", "both"], default="both")
+    ap.add_argument("--only", choices=["tx", "rx", "both", "chain"], default="both",
+                    help="chain: the bench's step (ChainPlan: the fused launch where it applies)")
     ap.add_argument("--amplitude", type=float, default=1.0)
     a = ap.parse_args()
     r = bench.GpuRunner(bench.WORKLOADS[a.config], 0, 0, amplitude=a.amplitude)
     for _ in range(a.reps):
+        if a.only == "chain":
+            r.step()
+            continue
         for c in range(r.nch):
             if a.only in ("tx", "both"):
                 r.tx(c)
