@@ -705,7 +705,7 @@ struct RxMfma {
 
     // The workgroup's tiles t_i = first + i * step (i < count, step = -grid: top-down), walked
     // with running values so that a tile's scalar bookkeeping is a few adds, not 64-bit
-    // multiplies and compares (the RX is issue-bound: 100 extra s_nop per tile cost it ~1.3 us,
+    // multiplies and compares (100 extra s_nop per tile cost the RX 0.4-0.7 us,
     // profiles/r03_sensitivity.txt): the tile, its window offset q = q_lo_of(t), and the
     // number of leading tiles on the fast path (q and t only decrease along the walk, so the
     // tiles with q >= 0 and t * TS >= lead come first).
