@@ -143,7 +143,7 @@ class GpuRunner:
 
     def fused(self):
         """1 when the last step ran as one launch per channel (modem_chain_fused), else 0."""
-        return 1 if self._plans and self._plans[0].fused == 1 else 0
+        return self._plans[0].fused if self._plans and self._plans[0].fused > 0 else 0
 
     def _tx_all(self):
         if self.batch:

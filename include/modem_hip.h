@@ -272,9 +272,11 @@ modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits,
                                 void* samples, size_t cap, void* out_iq, uint8_t* out_sym,
                                 size_t out_cap, modem_chain** out);
 modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_out, void* stream);
-/* How the last modem_chain_run ran: 1 = one launch (the TX and RX of the period fused: the
- * common filters, tile geometry permitting; results identical), 0 = the two launches, -1 = no
- * run yet or c == NULL. MODEM_CHAIN_FUSED=0 in the environment at create time forces 0. */
+/* How the last modem_chain_run ran: 1 or 2 = one launch (the TX and RX of the period fused:
+ * small calls with the common filters, tile geometry permitting; 2 = the form with one RX tile
+ * per workgroup that hands the samples over in LDS; results identical either way), 0 = the two
+ * launches, -1 = no run yet or c == NULL. MODEM_CHAIN_FUSED=0 in the environment at create time
+ * forces 0. */
 int modem_chain_fused(const modem_chain* c);
 modem_status modem_chain_destroy(modem_chain* c);
 

@@ -970,7 +970,8 @@ class ChainPlan:
 
     @property
     def fused(self) -> int:
-        """1: the last run() was one launch (TX and RX of the period fused), 0: two, -1: none."""
+        """1 or 2: the last run() was one launch (TX and RX of the period fused; 2: with the
+        samples handed over in LDS), 0: two launches, -1: no run yet."""
         return int(load_library().modem_chain_fused(self._h))
 
     def __del__(self):

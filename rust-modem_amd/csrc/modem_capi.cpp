@@ -1131,10 +1131,11 @@ modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_
         tx_fill(tx, c->bits, c->nbits, false, c->samples, nsym, ncarry_new, nsamp, tp);
         mk::RxParams rp{};
         rx_fill(rx, c->samples, nsamp, c->out_iq, c->out_sym, k_first, nout, rp);
+        int form = 1;
         const hipError_t e = mk::launch_chain_mfma(tp, (int)tx->sps, tx->mfma_ksteps, tx->d_bfrag, rp,
-                                                   rx->mfma_ksteps, rx->d_bfrag, tx->dtype, s);
+                                                   rx->mfma_ksteps, rx->d_bfrag, tx->dtype, s, &form);
         if (e == hipSuccess) {
-            c->last = 1;
+            c->last = form;
             tx_advance(tx, false, nsym, ncarry_new, nsamp);
             rx_advance(rx, nsamp);
             *produced = nsamp;

@@ -23,6 +23,10 @@
 
 namespace mk {
 
+// Which fused form the current launch_chain_mfma call took (1: chain_mfma, 2: chain_small);
+// set and read on the calling host thread only.
+static thread_local int g_chain_form = 1;
+
 struct ChainGeo {
     int64_t nrx;     // RX tiles of the call
     int64_t ntx;     // TX tiles of the call
@@ -92,6 +96,87 @@ void chain_mfma(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
     RK::template run<EM>(rp, pl, tbl, tables, red, sq, bid);
 }
 
+// The small call with one RX tile per workgroup (C2: 1024 tiles of 256 instants): the TX tile
+// and its tail sub-tiles are staged together (TxMfma::one_tile), every emitted sample is also
+// kept in an LDS window, and the RX stages its tile from there (RxMfma::run<EM, true>) instead of
+// draining the stores and reading them back from HBM; the RX tap tables and *ka_in are requested
+// at the kernel's start. LDS (halves): [TX planes x2 + LUT | RX planes] overlaid, then the RX
+// tables, the RX votes / maxima, then the sample window.
+template <int SPS, int NKS_T, int NKS_R>
+struct SmallLds {
+    using TK = TxMfma<SPS, NKS_T, OUT_IQ_MIXED, float, 1>;
+    using RK = RxMfma<SPS, NKS_R, float, MIX_COMPLEX, float, 1>;
+    static constexpr int TXH = 2 * TK::PLANES + 256 * 4;                 // + the largest LUT
+    static constexpr int A = ((TXH > 4 * RK::PL ? TXH : 4 * RK::PL) + 7) & ~7;
+    static constexpr int TBL = A, RED = A + RK::NC * 2 * RK::TB, RAW = (RED + 16 + 7) & ~7;
+    static size_t bytes(int raw_n) { return (size_t)(RAW + 4 * raw_n) * 2; }
+};
+
+template <int SPS, int NKS_T, int NKS_R, int EM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<SPS, NKS_R, float, MIX_COMPLEX, float, 1>::WPE)))
+void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParams rp,
+                 const _Float16* __restrict__ tables, const ChainGeo g) {
+    using L = SmallLds<SPS, NKS_T, NKS_R>;
+    using TK = typename L::TK;
+    using RK = typename L::RK;
+    extern __shared__ __attribute__((aligned(16))) _Float16 lds_s[];
+    const int64_t bid = blockIdx.x, nb = gridDim.x, t = bid;
+    if (bid == 0) tx_state_update(tp);
+    // the RX's tap tables and staging exponent, requested first
+    constexpr int NTB = RK::K_TAB8 / 256 + (RK::K_TAB8 % 256 ? 1 : 0);
+    h8 tv[NTB];
+#pragma unroll
+    for (int k = 0; k < NTB; ++k) {
+        const int j = threadIdx.x + k * 256;
+        if (j < RK::K_TAB8) tv[k] = reinterpret_cast<const h8*>(tables)[j];
+    }
+    const int kin = *rp.ka_in;
+    float2* raw = reinterpret_cast<float2*>(lds_s + L::RAW);
+    const int64_t rb = (t * TK::TS - tp.lead) * SPS - (int64_t)g.xs * (16 * TK::SB * SPS);
+    const int rn = g.xs * (16 * TK::SB * SPS) + TK::TS * SPS;
+    const RawOut ro{raw, rb, rn};
+    {
+        _Float16* pl = lds_s;
+        _Float16* pl2 = lds_s + TK::PLANES;
+        th4* lut_s = reinterpret_cast<th4*>(lds_s + 2 * TK::PLANES);
+        const int lane = threadIdx.x & 63;
+        th8 bh[NKS_T], bl[NKS_T];
+#pragma unroll
+        for (int s = 0; s < NKS_T; ++s) {
+            bh[s] = bfrag[(2 * s) * 64 + lane];
+            bl[s] = bfrag[(2 * s + 1) * 64 + lane];
+        }
+        bool done = false;
+        if (tp.fast_bits && tp.exact_idx) {
+            done = true;
+            switch (tp.bps) {
+            case 1: TK::template one_tile<1>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro); break;
+            case 2: TK::template one_tile<2>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro); break;
+            case 4: TK::template one_tile<4>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro); break;
+            case 8: TK::template one_tile<8>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro); break;
+            default: done = false;
+            }
+        }
+        if (!done) TK::template one_tile<0>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro);
+        // TX tiles past the last RX tile (their samples only feed the RX history)
+        if (bid == nb - 1 && g.ntx > g.nrx) TK::template run<0>(tp, pl, lut_s, bh, bl, g.nrx, g.ntx, 1, 0);
+    }
+    _Float16* tbl = lds_s + L::TBL;
+#pragma unroll
+    for (int k = 0; k < NTB; ++k) {
+        const int j = threadIdx.x + k * 256;
+        if (j < RK::K_TAB8) reinterpret_cast<h8*>(tbl)[j] = tv[k];
+    }
+    if (bid == nb - 1) {                       // the RX history reads HBM: this workgroup's stores first
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        rx_state_update<float>(rp);
+    }
+    const TileSeq sq{t, -1, 1, g.nrx};
+    RK::template run<EM, true>(rp, lds_s, tbl, tables, reinterpret_cast<float*>(lds_s + L::RED), sq, bid,
+                               RxHandoff{raw, rb, rn, kin});
+}
+
 // Launch geometry, or false when the call does not fit the fused form (the caller then runs
 // the two launches): matching tile sizes (small or not on both sides), RX tiles of m whole
 // TX tiles, every RX window inside [its TX tiles' start - 256 xs, their end), the RX history
@@ -144,6 +229,26 @@ static hipError_t chain_go_em(const TxParams& tp, const void* bfrag, const RxPar
     return hipGetLastError();
 }
 
+template <int SPS, int NKS_T, int NKS_R, int EM>
+static hipError_t chain_small_go(const TxParams& tp, const void* bfrag, const RxParams& rp, const void* tables,
+                                 hipStream_t s) {
+    using L = SmallLds<SPS, NKS_T, NKS_R>;
+    using RK = typename L::RK;
+    const int64_t nrx = (rp.nout + (rp.k_first & 15) + RK::TS - 1) / RK::TS;
+    ChainGeo g{};
+    if (!chain_geo<SPS, NKS_T, NKS_R, float, 1>(tp, rp, nrx, g) || g.m != 1) return hipErrorNotSupported;
+    const size_t lds = L::bytes(g.xs * (16 * L::TK::SB * SPS) + L::TK::TS * SPS);
+    const void* k = reinterpret_cast<const void*>(&chain_small<SPS, NKS_T, NKS_R, EM>);
+    if ((int64_t)persistent_grid(k, 256, lds, nrx) < nrx) return hipErrorNotSupported;   // one tile each, all resident
+#ifdef MODEM_CHAIN_PROBE
+    if (const char* e = std::getenv("MODEM_CHAIN_PROBE")) if (std::atoi(e) & 64) return hipErrorNotSupported;
+#endif
+    hipLaunchKernelGGL((chain_small<SPS, NKS_T, NKS_R, EM>), dim3((unsigned)nrx), dim3(256), lds, s, tp,
+                       static_cast<const th8*>(bfrag), rp, static_cast<const _Float16*>(tables), g);
+    g_chain_form = 2;
+    return hipGetLastError();
+}
+
 // Small calls only (both sides on their small tiles: one 16x16 sub-tile per wave), and the
 // steady-state epilogues only (the general one stays on the two launches). Small calls are
 // latency-bound and the fused launch saves a launch and the TX grid's drain (C2 chain 11.2 vs
@@ -158,6 +263,10 @@ static hipError_t chain_go(const TxParams& tp, const void* bfrag, const RxParams
     constexpr bool f32 = std::is_same<T, float>::value;
     auto go = [&](auto emc) -> hipError_t {
         constexpr int E = decltype(emc)::value;
+        if constexpr (f32) {                   // one RX tile per workgroup: the LDS hand-off form
+            const hipError_t e = chain_small_go<SPS, NKS_T, NKS_R, E>(tp, bfrag, rp, tables, s);
+            if (e != hipErrorNotSupported) return e;
+        }
         return chain_go_em<SPS, NKS_T, NKS_R, T, 1, E>(tp, bfrag, rp, tables, s);
     };
     switch (rx_mfma_em<T, MIX_COMPLEX, T>(rp)) {
@@ -180,7 +289,8 @@ static hipError_t chain_go(const TxParams& tp, const void* bfrag, const RxParams
 #define CHAIN_TABLE(X) X(4, 1, 4) X(4, 2, 6) X(8, 3, 20)
 
 hipError_t launch_chain_mfma(const TxParams& tp, int sps, int nks_t, const void* bfrag, const RxParams& rp,
-                             int nks_r, const void* tables, int dtype, hipStream_t s) {
+                             int nks_r, const void* tables, int dtype, hipStream_t s, int* form) {
+    g_chain_form = 1;
     auto sel = [&](auto tv) -> hipError_t {
         using T = decltype(tv);
 #define CHN(S, NT_, NR_) \
@@ -190,10 +300,12 @@ hipError_t launch_chain_mfma(const TxParams& tp, int sps, int nks_t, const void*
         return hipErrorNotSupported;
     };
 #ifdef MODEM_DEV_MIN
-    return dtype != 0 ? hipErrorNotSupported : sel(float());
+    const hipError_t e = dtype != 0 ? hipErrorNotSupported : sel(float());
 #else
-    return dtype == 1 ? sel(__half()) : sel(float());
+    const hipError_t e = dtype == 1 ? sel(__half()) : sel(float());
 #endif
+    if (form) *form = g_chain_form;
+    return e;
 }
 
 }  // namespace mk

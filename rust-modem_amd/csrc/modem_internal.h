@@ -150,9 +150,10 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
                      hipStream_t s);
 // One loopback period (TX into the sample buffer rp.x == tp.out, then RX over it, complex
 // mix, in and out of one dtype) as one persistent launch (modem_chain.hip); hipErrorNotSupported
-// when the filters or the call's geometry have no fused form (run the two launches then).
+// when the filters or the call's geometry have no fused form (run the two launches then);
+// *form = 1 (chain_mfma) or 2 (chain_small: one RX tile per workgroup, LDS hand-off).
 hipError_t launch_chain_mfma(const TxParams& tp, int sps, int nks_t, const void* bfrag, const RxParams& rp,
-                             int nks_r, const void* tables, int dtype, hipStream_t s);
+                             int nks_r, const void* tables, int dtype, hipStream_t s, int* form);
 hipError_t launch_fir(const FirParams& p, hipStream_t s);
 hipError_t launch_phases(float w, uint64_t s0, size_t n, float* out, hipStream_t s);
 hipError_t launch_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, hipStream_t s);

@@ -277,6 +277,15 @@ __device__ __forceinline__ int f32_exp(float m) { return (int)((__float_as_uint(
 // call's ntiles.
 struct TileSeq { int64_t first, step, count, ntiles; };
 
+// The fused small call's hand-off (RxMfma::run<EM, true>): the LDS copy of the samples the
+// workgroup's TX emitted, call samples [base, base + n), and the value of *ka_in.
+struct RxHandoff {
+    const float2* raw;
+    int64_t base;
+    int n;
+    int kin;
+};
+
 // Buffer descriptor over `bytes` bytes at `base` (wave-uniform inputs made provably uniform).
 // Accesses past `bytes` load zeros / are dropped without touching memory.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
@@ -800,9 +809,13 @@ struct RxMfma {
         }
     }
 
-    template <int EM>
+    // HO (the fused small call, modem_chain.hip): the tap tables are already in LDS, `ho.kin`
+    // holds *p.ka_in, and a first tile on the fast path reads its window from the LDS copy of
+    // the samples this workgroup's TX emitted (ho.raw) instead of from HBM; the general path,
+    // which reads HBM, first drains this workgroup's sample stores.
+    template <int EM, bool HO = false>
     __device__ __forceinline__ static void run(const RxParams& p, _Float16* pl, _Float16* tbl, const _Float16* __restrict__ tables,
-                               float* red, const TileSeq sq, int64_t bid) {
+                               float* red, const TileSeq sq, int64_t bid, const RxHandoff& ho = RxHandoff{}) {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         RX_STAMP(7, 0);
         const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
@@ -820,22 +833,43 @@ struct RxMfma {
         // memory latencies at the kernel's start overlap (the table stores wait for the table
         // loads only)
         constexpr int NTB = K_TAB8 / NT + (K_TAB8 % NT ? 1 : 0);
-        h8 tv[NTB];
-#pragma unroll
-        for (int k = 0; k < NTB; ++k) {
-            const int j = tid_() + k * NT;
-            if (j < K_TAB8) tv[k] = reinterpret_cast<const h8*>(tables)[j];
-        }
         const bool f0 = w.full();
-        prefetch(w.q, f0);
+        if constexpr (HO) {
+            static_assert(std::is_same<InT, float>::value, "LDS hand-off: f32 samples");
+            if (!f0) {
 #pragma unroll
-        for (int k = 0; k < NTB; ++k) {
-            const int j = tid_() + k * NT;
-            if (j < K_TAB8) reinterpret_cast<h8*>(tbl)[j] = tv[k];
+                for (int u = 0; u < U; ++u) pre[u] = QT{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+            } else {                           // the window from the LDS copy (zeros past it and the call)
+                const int e = 4 * tid_();
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    float2 x[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int eu = e + 4 * NT * u + j;
+                        const int64_t i = w.q + eu - ho.base;
+                        x[j] = eu < 4 * NQ && w.q + eu < p.N && i >= 0 && i < ho.n ? ho.raw[i] : make_float2(0.f, 0.f);
+                    }
+                    pre[u] = QT{make_float4(x[0].x, x[0].y, x[1].x, x[1].y), make_float4(x[2].x, x[2].y, x[3].x, x[3].y)};
+                }
+            }
+        } else {
+            h8 tv[NTB];
+#pragma unroll
+            for (int k = 0; k < NTB; ++k) {
+                const int j = tid_() + k * NT;
+                if (j < K_TAB8) tv[k] = reinterpret_cast<const h8*>(tables)[j];
+            }
+            prefetch(w.q, f0);
+#pragma unroll
+            for (int k = 0; k < NTB; ++k) {
+                const int j = tid_() + k * NT;
+                if (j < K_TAB8) reinterpret_cast<h8*>(tbl)[j] = tv[k];
+            }
         }
         __syncthreads();
         // the first prediction: where the previous call ended (any exponent tile_ka can give)
-        const int kin = *p.ka_in;
+        const int kin = HO ? ho.kin : *p.ka_in;
         int kpred = kin >= -120 && kin <= 120 && (kin & 7) == 0 ? kin : 0;
         if (f0 && kin == INT32_MIN) {          // a stream's first call: from the first tile's raw input
             float mx = 0.f;
@@ -866,6 +900,10 @@ struct RxMfma {
             else loop<true, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
             if (w.i < w.count) {               // tile w.t on the general path (one place in the code)
                 RX_STAMP(i, 6);
+                if constexpr (HO) {            // it reads HBM: this workgroup's sample stores first
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                }
                 kpred = slow_tile<EM>(p, pl, tbl, reds, w.t, cx.kb, cx.ld);
                 if (w.t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
                 RX_STAMP(i, 7);

@@ -122,6 +122,14 @@ __device__ __forceinline__ cf2 tx_cmix(cf2 y, cf2 cssn) {
 typedef _Float16 th8 __attribute__((ext_vector_type(8)));
 typedef _Float16 th4 __attribute__((ext_vector_type(4)));
 
+// An LDS copy of the samples a workgroup emits (the fused small call, modem_chain.hip: its RX
+// reads them there instead of from HBM): sample j of the call at p[j - base], 0 <= j - base < n.
+struct RawOut {
+    float2* p;
+    int64_t base;
+    int n;
+};
+
 template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB_ = 4>
 struct TxMfma {
     using C = TxMfmaCfg<SPS, SUB_>;
@@ -258,7 +266,9 @@ struct TxMfma {
     // Full 16x16 tile, carrier index < 2^53: unconditional stores. jt = call sample index of
     // the sub-tile's first sample. Per sample: packed unscale (2^-kab), bit-exact phase,
     // sin/cos, packed mix; stores through a uniform base + 32-bit lane offsets.
-    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
+    template <bool RAW = false>
+    __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale,
+                                     const RawOut& ro = RawOut{}) {
         const int lane = threadIdx.x & 63;
         int loff = 64 * (lane >> 4) + (lane & 15);          // sample of row r: loff + 16 r
         asm volatile("" : "+v"(loff));
@@ -285,6 +295,13 @@ struct TxMfma {
             z[3] = tx_cmix(z[3], (cf2){cs1.y, sn1.y});
         }
 #endif
+        if constexpr (RAW) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t i = jt + loff + 16 * r - ro.base;
+                if (i >= 0 && i < ro.n) ro.p[i] = make_float2(z[r].x, z[r].y);
+            }
+        }
 #ifdef MODEM_ABLATE_STORE
 #pragma unroll
         for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(z[r]));
@@ -305,7 +322,9 @@ struct TxMfma {
 
     // Partial tile, samples before the call, or carrier index >= 2^53: guarded, 64-bit
     // indices; the same arithmetic as emit_full (a sample's bits never depend on the path).
-    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale) {
+    template <bool RAW = false>
+    __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale,
+                                     const RawOut& ro = RawOut{}) {
         const int lane = threadIdx.x & 63;
         const int64_t jend = p.nsym * SPS;
 #pragma unroll
@@ -317,6 +336,10 @@ struct TxMfma {
                 float sn, cs;
                 sincos_phase(carrier_phase_off(p.w, p.s0 + (uint64_t)jt, off, p.exact_idx), sn, cs);
                 z = tx_cmix(z, (cf2){cs, sn});
+            }
+            if constexpr (RAW) {
+                const int64_t i = jt + off - ro.base;
+                if (i >= 0 && i < ro.n) ro.p[i] = make_float2(z.x, z.y);
             }
             if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, jt + off, z.x);
             else OutIO<OutT>::store_one(p.out, jt + off, z.x, z.y);
@@ -340,6 +363,86 @@ struct TxMfma {
             if (p.levels) fir<true>(pl, q, bh, bl, dre, dim);
             else fir<false>(pl, q, bh, bl, dre, dim);
             emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
+        }
+        __syncthreads();                                            // the planes are restaged next
+    }
+
+    // One tile t and, before it, the last xs sub-tiles of tile t - 1 (the fused small call,
+    // modem_chain.hip: one RX tile per workgroup). The tail's symbol loads fly with the tile's
+    // and the LUT's, both are staged before one barrier (the tail into the second plane set
+    // pl2), and every emitted sample is also written to the LDS window `ro`.
+    template <int BPS>
+    __device__ __forceinline__ static void one_tile(const TxParams& p, _Float16* pl, _Float16* pl2, th4* lut_s,
+                                                    const th8 (&bh)[NKS], const th8 (&bl)[NKS], int64_t t, int xs,
+                                                    const RawOut& ro) {
+        constexpr int NK = (NE + NT - 1) / NT;
+        const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int kab = p.lut_scale_exp + p.tap_scale_exp;
+        const float us = __builtin_ldexpf(1.0f, -kab);
+        const cf2 unscale = {us, us};
+        const int64_t ms = t * TS - p.lead - PRE, mlast = p.nsym_valid - 1;
+        const bool fullt = BPS > 0 && ms >= 0 && ms + NE <= p.nsym_valid && t * TS - p.lead + TS <= p.nsym;
+        uint64_t pre[U];
+        if (fullt) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int64_t m = ms + tid + NT * u;
+                m = m < 0 ? 0 : (m > mlast ? mlast : m);
+                pre[u] = load_word<BPS>(p.bits, m);
+            }
+        }
+        const bool tl = xs > 0 && t > 0;
+        const int g0 = 4 * SUB - xs, e_lo = g0 * 16 * SB;
+        const int64_t ms2 = ms - TS;
+        uint32_t idx[NK];
+        float2 hv[NK];
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int e = tid + k * NT;
+            const int64_t m = ms2 + e;
+            idx[k] = 0;
+            hv[k] = make_float2(0.f, 0.f);
+            if (tl && e < NE && e >= e_lo) {
+                if (m < 0) { if (m >= -(int64_t)(p.K - 1)) hv[k] = p.hist[m + p.K - 1]; }
+                else if (m < p.nsym_valid) idx[k] = tx_symbol_index(p, m);
+            }
+        }
+        const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
+        for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = lut_h[i];
+        __syncthreads();   // LUT visible
+        if (fullt) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int e = tid + NT * u;
+                if (e < NE) put(pl, e, lut_s[word_index(pre[u], BPS)]);
+            }
+        } else {
+            stage_slow(p, pl, lut_s, ms);
+        }
+        if (tl) {
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int e = tid + k * NT;
+                const int64_t m = ms2 + e;
+                if (e < NE && e >= e_lo) put(pl2, e, m >= 0 && m < p.nsym_valid ? lut_s[idx[k]] : split_value(p, hv[k]));
+            }
+        }
+        __syncthreads();
+        const int64_t j0 = (t * TS - p.lead) * SPS, j2 = j0 - (int64_t)TS * SPS;
+        const bool lv = p.levels != 0;
+#pragma unroll 1
+        for (int q = 0; q < SUB; ++q) {
+            const int g = wave * SUB + q;
+            f32x4 dre, dim;
+            if (tl && g >= g0) {                                    // wave-uniform
+                if (lv) fir<true>(pl2, q, bh, bl, dre, dim);
+                else fir<false>(pl2, q, bh, bl, dre, dim);
+                emit_edge<true>(p, j2 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
+            }
+            if (lv) fir<true>(pl, q, bh, bl, dre, dim);
+            else fir<false>(pl, q, bh, bl, dre, dim);
+            if (fullt) emit_full<true>(p, j0 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
+            else emit_edge<true>(p, j0 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
         }
         __syncthreads();                                            // the planes are restaged next
     }

@@ -91,9 +91,11 @@ def test_fused_chain_equals_two_launches(m, o, torch_cuda, cfg, dtype, nsym, ext
         assert torch.equal(s1[:k1], s2[:k2]), f"period {p}: decisions differ"
         assert txf.carrier.sample == txt.carrier.sample and rxf.carrier.sample == rxt.carrier.sample
     if want == 1:
-        assert all(h == 1 for h in how[1:]), how
+        assert all(h >= 1 for h in how[1:]), how
     elif want == 0:
         assert not any(how), how
+    if want == 1 and dtype == 0 and sps == 4:   # one RX tile per workgroup: the LDS hand-off form
+        assert all(h == 2 for h in how[1:]), how
     print(f"\n[fused] {cfg} dtype {dtype} nsym {nsym}+{extra}b: fused per period {how}")
     # the last period's decisions are the symbols of the continuing stream
     nsym_p = (nb + 0) // bps
