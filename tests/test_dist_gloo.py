@@ -77,7 +77,7 @@ def _worker(rank, world, port, outdir):
     td.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     bench.WORKLOADS["tiny"] = ("qam16", 4, 129, 4, 1 << 12, 2, 0, "tiny: 2 channels x 4096 samples")
     args = bench.argparse.Namespace(config="tiny", steps=3, warmup=1, no_cpu_baseline=True, cpu_samples=0,
-                                    amplitude=1.0, no_out_of_cache=True)
+                                    amplitude=1.0, no_out_of_cache=True, settle_ms=0.0)
     runners = []
 
     def factory(wl, r):
