@@ -558,6 +558,20 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
     return MODEM_OK;
 }
 
+// Non-temporal TX stores for large launches. A launch writing more than the Infinity Cache
+// holds (256 MiB on MI355X) streams its samples through it to HBM anyway, and its dirty lines
+// are then written back while the RX reads the buffer. Such a launch (over 192 MiB: C5, 512
+// MiB) stores its samples non-temporally, straight to HBM: C5 chain 273.4 -> 257.9 us, the TX
+// 130.4 -> 104.0 us, the RX after it 143.0 -> 153.9 us (profiles/r03_tx_nt.txt; keeping the
+// last 128 MiB cacheable for the RX measured 261.4). Smaller launches (C3: 128 MiB, whose RX
+// re-reads it from the cache) keep the default policy. MODEM_TX_NT=0 turns it off (A/B).
+// `launch_bytes`: the whole launch's output (every channel of a batch); returns nt_below.
+static int64_t tx_nt_below(int64_t nsamp, uint64_t launch_bytes) {
+    static const int mode = [] { const char* e = std::getenv("MODEM_TX_NT"); return e ? std::atoi(e) : 1; }();
+    constexpr uint64_t kMin = 192ull << 20;
+    return mode != 0 && launch_bytes > kMin && nsamp > 0 ? nsamp : 0;
+}
+
 // Kernel parameters of one TX call on device buffers (dbits, dout); see tx_run.
 static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool flush, void* dout,
                     int64_t nsym, int ncarry_new, size_t nsamp, mk::TxParams& p) {
@@ -570,6 +584,7 @@ static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool 
     p.taps = h->d_taps;
     p.taps_q = h->d_taps_q;
     p.out = dout;
+    p.nt_below = tx_nt_below((int64_t)nsamp, (uint64_t)nsamp * tx_sample_bytes(h));
     p.s0 = h->sample;
     p.nsym = nsym;
     p.nsym_valid = flush ? 0 : nsym;
@@ -730,6 +745,11 @@ modem_status modem_tx_process_batch(modem_tx* const* hs, size_t nch, const uint8
             const size_t c = c0 + (size_t)i;
             tx_fill(hs[c], bits[c], nbits[c], false, outs[c], nsym[c], ncarry_new[c], (size_t)nsym[c] * hs[c]->sps, b.p[i]);
         }
+        uint64_t launch_bytes = 0;          // the non-temporal split over the whole launch
+        for (int i = 0; i < b.nch; ++i)
+            launch_bytes += (uint64_t)nsym[c0 + i] * hs[c0 + i]->sps * tx_sample_bytes(hs[c0 + i]);
+        for (int i = 0; i < b.nch; ++i)
+            b.p[i].nt_below = tx_nt_below(nsym[c0 + i] * (int64_t)hs[c0 + i]->sps, launch_bytes);
         HIP_TRY(mk::launch_tx_mfma_batch(b, (int)hs[0]->sps, hs[0]->mfma_ksteps, hs[0]->d_bfrag, hs[0]->dtype, s));
         for (int i = 0; i < b.nch; ++i) {
             const size_t c = c0 + (size_t)i;

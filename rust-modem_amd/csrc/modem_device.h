@@ -130,6 +130,10 @@ template <> struct OutIO<float> {
     __device__ static void store_one(void* out, int64_t j, float a, float b) {
         *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + 2 * j) = make_float2(a, b);
     }
+    __device__ static void store_one_nt(void* out, int64_t j, float a, float b) {   // non-temporal
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store((v2f){a, b}, reinterpret_cast<v2f*>(reinterpret_cast<float*>(out) + 2 * j));
+    }
     __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
         *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + j) = make_float2(a, b);
     }
@@ -147,6 +151,11 @@ template <> struct OutIO<__half> {
     }
     __device__ static void store_one(void* out, int64_t j, float a, float b) {
         *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + 2 * j) = __floats2half2_rn(a, b);
+    }
+    __device__ static void store_one_nt(void* out, int64_t j, float a, float b) {   // non-temporal
+        const __half2 h = __floats2half2_rn(a, b);
+        __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&h),
+                                    reinterpret_cast<uint32_t*>(reinterpret_cast<__half*>(out) + 2 * j));
     }
     __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
         *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + j) = __floats2half2_rn(a, b);

@@ -18,6 +18,7 @@ struct TxParams {
     const float* taps;       // polyphase taps, taps[t*sps + p] = h[p + sps*t], K*sps floats
     const float* taps_q;     // Q-rail taps (the I taps delayed by the Q offset), or null: = taps
     void* out;               // f32 or f16 samples (layout per out_mode)
+    int64_t nt_below;        // tx_mfma: full sub-tiles of call samples < nt_below store non-temporally
     uint64_t s0;             // carrier sample of output sample 0
     int64_t nsym;            // symbols this call emits
     int64_t nsym_valid;      // symbols < nsym_valid are data, the rest are zero (flush)

@@ -311,11 +311,17 @@ struct TxMfma {
         const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
         char* ob = reinterpret_cast<char*>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(oa >> 32)) << 32) |
                                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)oa));
+        if (OUT_MODE != OUT_REAL && jt < p.nt_below) {     // uniform: past the Infinity Cache (tx_nt_below)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            char* q = ob + (uint32_t)((loff + 16 * r) * SBYTES);
-            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(q, 0, z[r].x);
-            else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
+            for (int r = 0; r < 4; ++r)
+                OutIO<OutT>::store_one_nt(ob + (uint32_t)((loff + 16 * r) * SBYTES), 0, z[r].x, z[r].y);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                char* q = ob + (uint32_t)((loff + 16 * r) * SBYTES);
+                if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(q, 0, z[r].x);
+                else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
+            }
         }
 #endif
     }

@@ -1,0 +1,62 @@
+"""Non-temporal TX stores (rust-modem_amd/csrc/modem_capi.cpp tx_nt_below): a TX launch whose
+output exceeds 192 MiB (past the 256 MiB Infinity Cache) stores its samples non-temporally.
+The store policy must not change a single sample:
+
+  * C5's filter (256-QAM, 513 taps, sps 8) over 2^25 samples (256 MiB of f32 I/Q: the
+    non-temporal form) equals, bit for bit, the same stream produced by two calls of 2^24
+    samples (128 MiB each: the default policy), and the RX decisions over it equal the symbols
+    sent (modulator.rs:85-100, fir.rs:18-34; the loopback property of SURVEY.md §8c);
+  * a 2^16-sample window deep in the call against the oracle's TX chain at that carrier index,
+    within 4e-5 of max (the 513-tap bound of tests/test_gpu_parity.py).
+"""
+import numpy as np
+import pytest
+
+from conftest import CONFIGS, oracle_phasor, sent_symbols
+
+pytestmark = pytest.mark.gpu
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+def test_large_call_nontemporal_equals_split_calls(m, o, torch_cuda):
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS["c5_qam256"]
+    N = 1 << 25
+    nsym = N // sps
+    w = o.sample_freq(1, 4)
+    taps = m.rrc_taps(L, sps, 0.35)
+    bits = m.prng_bits(0x5EED2000, nsym * bps)
+    one = m.DigitalModulator(m.Carrier(w), m.QAM(8, 0.0, 1.0), sps, taps)
+    two = m.DigitalModulator(m.Carrier(w), m.QAM(8, 0.0, 1.0), sps, taps)
+    y1 = torch.empty((N, 2), dtype=torch.float32, device="cuda")
+    y2 = torch.empty((N, 2), dtype=torch.float32, device="cuda")
+    one.process(bits, out=y1)                                    # 256 MiB: non-temporal stores
+    half = nsym // 2 * bps
+    two.process(bits[:half], out=y2[: N // 2])                   # 2 x 128 MiB: default policy
+    two.process(bits[half:], out=y2[N // 2:])
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2), "the non-temporal call's samples differ from the split calls'"
+    # the oracle's TX chain over a window deep in the call (stream sample A = K sps)
+    K = nsym - 3 * (1 << 13)
+    A, WIN = K * sps, 1 << 16
+    H = (L - 1 + sps - 1) // sps
+    hb = host(bits)
+    seg = hb[(K - H) * bps:(K + WIN // sps) * bps]
+    ref = o.tx_chain(oracle_phasor(o, name), seg, sps, taps, w, (K - H) * sps)[H * sps:]   # [A, A + WIN)
+    ref = np.asarray(ref, dtype=np.float64)
+    assert ref.shape == (WIN, 2)
+    got = host(y1[A: A + WIN]).astype(np.float64)
+    err = float(np.abs(got - ref).max() / np.abs(ref).max())
+    print(f"\n[nt] C5 2^25 TX window at {A}: max rel err {err:.3g}")
+    assert err <= 4e-5
+    # the RX over the non-temporal samples decides the symbols sent
+    rx = m.DemodulatorRx(m.Carrier(w), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                         slicer=m.QAM(8, 0.0, 1.0).slicer())
+    _, sym = rx.process(y1)
+    torch.cuda.synchronize()
+    sent = sent_symbols(hb, bps)
+    got_sym = host(sym)
+    assert np.array_equal(got_sym, sent[: got_sym.shape[0]])

@@ -14,5 +14,5 @@ for c in "$@"; do
   echo "== $label [$envs] [$var] rc=$rc $(grep -E '^ok' gpurun_out/ab_$label.log)"
   case $rc in 124|134|137|139) exit $rc;; esac
   [ $rc -ne 0 ] && { tail -5 gpurun_out/ab_$label.log; exit $rc; }
-  grep -E "tx_mfma|rx_mfma|tx_fast|chain_mfma" gpurun_out/ab_$label/run_kernel_stats.csv | awk -F'",' '{split($2,a,","); printf "   %-40s n %5d avg %8.2f us  min %8.2f\n", substr($1,2,40), a[1], a[3]/1000, a[5]/1000}'
+  grep -E "tx_mfma|rx_mfma|rx_ring|tx_fast|chain_mfma" gpurun_out/ab_$label/run_kernel_stats.csv | awk -F'",' '{split($2,a,","); printf "   %-40s n %5d avg %8.2f us  min %8.2f\n", substr($1,2,40), a[1], a[3]/1000, a[5]/1000}'
 done
