@@ -7,7 +7,9 @@ A step is one pass of the hot path over one batch: bits (device-resident, one by
 I/Q + u8 decisions. Workload per GPU is BASELINE config 3 (16-QAM, 129-tap RRC, sps 4,
 16 M samples); with --gpus N each rank runs its own independent channel (weak scaling, no
 data-path collective — SURVEY.md §8e). `value` = samples processed by all ranks / the max
-over ranks of the timed region.
+over ranks of the timed region. Before the warmup each rank runs --settle-ms (300) of untimed
+back-to-back steps: the device clock dips for the first ~100 ms of sustained load, and the
+driver's 20-step region (~1.2 ms) would otherwise measure that transient (tools/region_probe.py).
 
 Also reported: the dominant kernel's HBM roofline (algorithmic bytes per launch / its mean
 duration from HIP events on the launch stream; peak 8 TB/s), the whole chain's roofline,
