@@ -167,3 +167,30 @@ def test_cpu_baseline_multicore_leg():
     assert out["single_thread"]["cores"] == 1 and out["single_thread"]["value"] > 0
     assert "2 threads x 8192 samples" in out["sample"]
     assert 1 <= bench._cpu_threads() <= 16
+
+
+def test_settle_clocks_runs_untimed_steps_for_the_budget():
+    """bench.settle_clocks: back-to-back steps until the wall-clock budget is spent, synchronising
+    after each batch (the queue drains only between batches), batches sized from the measured
+    step rate; 0 ms runs nothing. It happens before the warmup, outside the timed region."""
+    import bench
+
+    class R:
+        def __init__(self):
+            self.steps = self.syncs = 0
+
+        def step(self):
+            self.steps += 1
+            time.sleep(0.0005)
+
+        def sync(self):
+            self.syncs += 1
+
+    r = R()
+    assert bench.settle_clocks(r, 0) is None and r.steps == 0
+    t0 = time.perf_counter()
+    out = bench.settle_clocks(r, 60.0)
+    dt = (time.perf_counter() - t0) * 1e3
+    assert out["steps"] == r.steps and r.steps >= 20
+    assert 60.0 <= out["ms"] <= dt + 1.0 and dt < 60.0 + 40.0     # batches end near the budget
+    assert r.syncs < r.steps                                      # steps are queued in batches
