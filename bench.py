@@ -337,6 +337,8 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
     # (tools/region_probe.py, profiles/r03_region_probe.txt); the driver's 20-step region
     # (~1.2 ms) otherwise measures where it falls in that transient, not the steady state the
     # metric is about. The timed region below is still exactly --steps full steps.
+    if dist is not None:
+        dist.barrier()      # the ranks settle together and reach the timing barrier together
     settle = settle_clocks(r, getattr(args, "settle_ms", 0.0))
     for _ in range(args.warmup):
         r.step()
@@ -427,9 +429,10 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
 
 
 def settle_clocks(r, settle_ms):
-    """Back-to-back steps for settle_ms of wall time, untimed, queued in batches of up to ~20 ms
-    of device work (so that the queue rarely drains; a batch is sized from the previous one's
-    rate). Returns what ran, for the JSON line."""
+    """Back-to-back steps for settle_ms of wall time, untimed, queued in batches of up to ~5 ms
+    of device work (the queue drains only between batches; a batch is sized from the previous
+    one's rate, so that ranks that start together end within ~5 ms of each other). Returns what
+    ran, for the JSON line."""
     if settle_ms <= 0:
         return None
     t0 = time.perf_counter()
@@ -445,7 +448,7 @@ def settle_clocks(r, settle_ms):
         if left <= 0:
             break
         per = max((now - tb) / batch, 1e-6)
-        batch = max(1, min(int(min(left, 0.02) / per) + 1, 100000))
+        batch = max(1, min(int(min(left, 0.005) / per) + 1, 100000))
     return {"ms": round((time.perf_counter() - t0) * 1e3, 1), "steps": n,
             "what": "untimed back-to-back steps before the warmup (device clock settling)"}
 
