@@ -91,9 +91,12 @@ class GpuRunner:
         for c in range(nch):
             seed = channel_seed(rank, nch, c)
             bits = m.prng_bits(seed, nbits, device=device)
-            tx = m.DigitalModulator(m.Carrier(w), ph(), sps, taps, dtype=dtype)
+            tx = m.DigitalModulator(m.Carrier(w), ph(), sps, taps, dtype=dtype, device=device)
             rx = m.DemodulatorRx(m.Carrier(w), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
-                                 slicer=ph().slicer(), in_dtype=dtype, out_dtype=dtype)
+                                 slicer=ph().slicer(), in_dtype=dtype, out_dtype=dtype, device=device)
+            # every handle of this rank lives on the rank's GPU (ranks that share one GPU in the
+            # tests would otherwise hide a handle left on device 0)
+            assert tx.device == device and rx.device == device, (tx.device, rx.device, device)
             tdt = torch.float16 if dtype == 1 else torch.float32
             y = torch.empty((nsamp, 2), dtype=tdt, device=f"cuda:{device}")
             nout = rx.noutputs(nsamp)
@@ -531,26 +534,72 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _spawn(args, argv):
+def _wait_ranks(procs, timeout_s, poll_s=0.2):
+    """Wait for every rank process. A rank that exits non-zero, or the overall timeout, ends the
+    rest (terminate, then kill); returns the exit codes (the timeout reports 124 for the ranks
+    it ended, as `timeout` does) and the code of the first rank seen failing (None if none)."""
+    t0 = time.monotonic()
+    rcs = [None] * len(procs)
+    failed = timed_out = False
+    first_bad = None
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+                if rcs[i] not in (None, 0):
+                    failed = True
+                    if first_bad is None:
+                        first_bad = rcs[i]
+        if failed or time.monotonic() - t0 > timeout_s:
+            timed_out = not failed
+            break
+        time.sleep(poll_s)
+    if failed or timed_out:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for i, p in enumerate(procs):
+            try:
+                p.wait(10)
+            except Exception:
+                p.kill()
+                p.wait()
+            if rcs[i] is None:
+                rcs[i] = 124 if timed_out else p.returncode
+    if timed_out:
+        first_bad = 124
+    return rcs, first_bad
+
+
+def _spawn(args, argv, timeout_s=1800.0):
     """--gpus N without a launcher: N fresh rank processes (`python bench.py` with RANK /
     LOCAL_RANK / WORLD_SIZE / MASTER_* set), started before this process touches the GPU (it
     never does). Rank 0's JSON line is printed and returned; the exit status is the worst of
-    the ranks'."""
+    the ranks'. All ranks are polled: when one exits non-zero the others are terminated (a rank
+    left waiting in a barrier for a dead peer would otherwise hang the bench), and the whole
+    run is bounded by `timeout_s`."""
     import subprocess
+    import tempfile
     env = dict(os.environ, WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     procs = []
+    # rank 0's stdout goes to a file, so that polling never blocks on a full pipe
+    out_f = tempfile.TemporaryFile(mode="w+")
     for r in range(args.gpus):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
-    out0 = procs[0].communicate()[0]
-    rcs = [p.wait() for p in procs]
+                                      stdout=out_f if r == 0 else subprocess.DEVNULL, text=True))
+    rcs, first_bad = _wait_ranks(procs, timeout_s)
+    out_f.seek(0)
+    out0 = out_f.read()
+    out_f.close()
     line = None
     for ln in (out0 or "").splitlines():
         if ln.startswith("{"):
             line = ln
     if line is not None:
         print(line, flush=True)
+    if first_bad is not None:
+        raise SystemExit(first_bad)
     bad = [rc for rc in rcs if rc != 0]
     if bad:
         raise SystemExit(bad[0])

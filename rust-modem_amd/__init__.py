@@ -946,6 +946,16 @@ class ChainPlan:
         self.bits, self.samples, self.out_iq, self.out_sym = bits, samples, out_iq, out_sym
         if tx.dtype != rx.in_dtype or tx.out_mode == OUT_REAL:
             raise ValueError("ChainPlan: the RX must read the TX's interleaved samples (one dtype)")
+        # the C side sizes every buffer from its first dimension: a buffer of the wrong width
+        # would be written past its end on the device
+        _check_rx_input(samples, tx.dtype, "ChainPlan samples")
+        want_out = _IN_DTYPE_NAME[rx.out_dtype]
+        if out_iq is not None and (len(out_iq.shape) != 2 or int(out_iq.shape[1]) != 2
+                                   or _dtype_name(out_iq) != want_out):
+            raise ValueError(f"ChainPlan: out_iq must be (k, 2) {want_out} (the RX's out_dtype), "
+                             f"got {tuple(out_iq.shape)} {_dtype_name(out_iq)}")
+        if out_sym is not None and (len(out_sym.shape) != 1 or _dtype_name(out_sym) != "uint8"):
+            raise ValueError(f"ChainPlan: out_sym must be (k,) uint8, got {tuple(out_sym.shape)} {_dtype_name(out_sym)}")
         self._nbits = int(bits.numel() if _is_torch(bits) else bits.size)
         caps = [int(x.shape[0]) for x in (out_iq, out_sym) if x is not None]
         h = ctypes.c_void_p()

@@ -561,9 +561,11 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
 // Non-temporal TX stores for large launches. A launch writing more than the Infinity Cache
 // holds (256 MiB on MI355X) streams its samples through it to HBM anyway, and its dirty lines
 // are then written back while the RX reads the buffer. Such a launch (over 192 MiB: C5, 512
-// MiB) stores its samples non-temporally, straight to HBM: C5 chain 273.4 -> 257.9 us, the TX
-// 130.4 -> 104.0 us, the RX after it 143.0 -> 153.9 us (profiles/r03_tx_nt.txt; keeping the
-// last 128 MiB cacheable for the RX measured 261.4). Smaller launches (C3: 128 MiB, whose RX
+// MiB) stores its samples non-temporally, straight to HBM. In-tree A/B of this host switch
+// (profiles/r03_tx_nt.txt, bench legs): C5 chain 280.9 -> 268.5 us, TX alone 135 -> 109 us,
+// the RX in the chain 145.5 -> 159.5 us (it now reads everything from HBM); C4 chain 121 ->
+// 116.6 us. (The earlier compile-time all-NT build measured C5 chain 273.4 -> 257.9 us on
+// another box; keeping the last 128 MiB cacheable, 261.4.) Smaller launches (C3: 128 MiB, whose RX
 // re-reads it from the cache) keep the default policy. MODEM_TX_NT=0 turns it off (A/B).
 // `launch_bytes`: the whole launch's output (every channel of a batch); returns nt_below.
 static int64_t tx_nt_below(int64_t nsamp, uint64_t launch_bytes) {

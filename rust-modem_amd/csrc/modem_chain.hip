@@ -32,8 +32,6 @@ struct ChainGeo {
     int64_t ntx;     // TX tiles of the call
     int32_t m;       // TX tiles per RX tile
     int32_t xs;      // sub-tiles of TX tile m r0 - 1 a workgroup recomputes (r0 > 0)
-    int32_t probe;   // experiment builds (-DMODEM_CHAIN_PROBE, env MODEM_CHAIN_PROBE): 1 no RX, 2 no TX,
-                     // 4 no tail sub-tiles, 8 TX tiles grid-strided (timing only: wrong RX input)
 };
 
 template <int SPS, int NKS_T, int NKS_R, typename T, int SUB, int EM>
@@ -45,17 +43,10 @@ void chain_mfma(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_c[];
     const int64_t bid = blockIdx.x, nb = gridDim.x;
     const int64_t r0 = g.nrx * bid / nb, r1 = g.nrx * (bid + 1) / nb;
-    int64_t t0 = r0 * g.m, t1 = bid == nb - 1 ? g.ntx : r1 * g.m, ts = 1;
-    int xs = g.xs;
-#ifdef MODEM_CHAIN_PROBE
-    if (g.probe & 4) xs = 0;
-    if (g.probe & 8) { t0 = bid; t1 = g.ntx; ts = nb; xs = 0; }
-#endif
+    const int64_t t0 = r0 * g.m, t1 = bid == nb - 1 ? g.ntx : r1 * g.m, ts = 1;
+    const int xs = g.xs;
     // ---- TX: tiles [t0, t1), after the last xs sub-tiles of tile t0 - 1
     if (bid == 0) tx_state_update(tp);
-#ifdef MODEM_CHAIN_PROBE
-    if (!(g.probe & 2))
-#endif
     {
         _Float16* pl = lds_c;
         th4* lut_s = reinterpret_cast<th4*>(lds_c + TK::PLANES);
@@ -86,9 +77,6 @@ void chain_mfma(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
     // workgroup (checked on the host)
     if (bid == nb - 1) rx_state_update<T>(rp);
     // ---- RX: tiles r1 - 1 down to r0 (the last written first)
-#ifdef MODEM_CHAIN_PROBE
-    if (g.probe & 1) return;
-#endif
     _Float16* pl = lds_c;
     _Float16* tbl = lds_c + 4 * RK::PL;
     float* red = reinterpret_cast<float*>(tbl + RK::NC * 2 * RK::TB);
@@ -216,14 +204,8 @@ static hipError_t chain_go_em(const TxParams& tp, const void* bfrag, const RxPar
     const int64_t lead_rx = rp.k_first & 15;
     const int64_t nrx = (rp.nout + lead_rx + RK::TS - 1) / RK::TS;
     unsigned grid = persistent_grid(k, 256, lds, nrx);
-#ifdef MODEM_CHAIN_PROBE
-    if (const char* e = std::getenv("MODEM_CHAIN_GRID_DIV")) grid = (grid + std::atoi(e) - 1) / std::atoi(e);
-#endif
     ChainGeo g{};
     if (!chain_geo<SPS, NKS_T, NKS_R, T, SUB>(tp, rp, grid, g)) return hipErrorNotSupported;
-#ifdef MODEM_CHAIN_PROBE
-    if (const char* e = std::getenv("MODEM_CHAIN_PROBE")) g.probe = std::atoi(e);
-#endif
     hipLaunchKernelGGL((chain_mfma<SPS, NKS_T, NKS_R, T, SUB, EM>), dim3(grid), dim3(256), lds, s, tp,
                        static_cast<const th8*>(bfrag), rp, static_cast<const _Float16*>(tables), g);
     return hipGetLastError();
@@ -240,9 +222,6 @@ static hipError_t chain_small_go(const TxParams& tp, const void* bfrag, const Rx
     const size_t lds = L::bytes(g.xs * (16 * L::TK::SB * SPS) + L::TK::TS * SPS);
     const void* k = reinterpret_cast<const void*>(&chain_small<SPS, NKS_T, NKS_R, EM>);
     if ((int64_t)persistent_grid(k, 256, lds, nrx) < nrx) return hipErrorNotSupported;   // one tile each, all resident
-#ifdef MODEM_CHAIN_PROBE
-    if (const char* e = std::getenv("MODEM_CHAIN_PROBE")) if (std::atoi(e) & 64) return hipErrorNotSupported;
-#endif
     hipLaunchKernelGGL((chain_small<SPS, NKS_T, NKS_R, EM>), dim3((unsigned)nrx), dim3(256), lds, s, tp,
                        static_cast<const th8*>(bfrag), rp, static_cast<const _Float16*>(tables), g);
     g_chain_form = 2;

@@ -94,10 +94,6 @@ __device__ __forceinline__ float carrier_phase_off(float w, uint64_t base, int o
 // the sample tolerance is set in tests/test_gpu_parity.py. (The bit-exact libm results of the
 // reference's own demodulator: libm_sincosf.h.)
 __device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
-#if defined(MODEM_ABLATE_TRIG)        // profiling builds only (tools/ablate.sh)
-    s = ph; c = 1.0f;
-    return;
-#endif
     s = __sinf(ph);
     c = __cosf(ph);
 }
@@ -105,14 +101,9 @@ __device__ __forceinline__ void sincos_phase(float ph, float& s, float& c) {
 // Hardware sin/cos of two phases (what __sinf/__cosf compile to: v_sin/v_cos of phase/2pi,
 // here with one packed multiply for both samples).
 __device__ __forceinline__ void sincos_phase2(cf2 ph, cf2& s, cf2& c) {
-#if defined(MODEM_ABLATE_TRIG)
-    sincos_phase(ph.x, s.x, c.x);
-    sincos_phase(ph.y, s.y, c.y);
-#else
     const cf2 rev = ph * kRcp2Pi;
     s = (cf2){__builtin_amdgcn_sinf(rev.x), __builtin_amdgcn_sinf(rev.y)};
     c = (cf2){__builtin_amdgcn_cosf(rev.x), __builtin_amdgcn_cosf(rev.y)};
-#endif
 }
 
 typedef const __attribute__((address_space(4))) float cfloat;   // wave-uniform -> s_load
@@ -232,11 +223,6 @@ static inline unsigned persistent_grid(const void* kernel, int threads, size_t l
 template <int NKS, int PD, typename OffF>
 __device__ __forceinline__ void mfma_chain(const float2* arow, OffF off, const float (&bf)[NKS],
                                            f32x4& dre, f32x4& dim) {
-#ifdef MODEM_ABLATE_FIR
-    const float2 a0 = arow[off(0)];
-    dre[0] += a0.x * bf[0]; dim[0] += a0.y * bf[NKS - 1];
-    return;
-#endif
     float2 a[PD];
 #pragma unroll
     for (int s = 0; s < PD && s < NKS; ++s) a[s] = arow[off(s)];
@@ -255,11 +241,6 @@ __device__ __forceinline__ void mfma_chain(const float2* arow, OffF off, const f
 template <int NKS, int PD, typename OffF>
 __device__ __forceinline__ void mfma_chain_lb(const float2* arow, OffF off, const float* brow,
                                               f32x4& dre, f32x4& dim) {
-#ifdef MODEM_ABLATE_FIR
-    const float2 a0 = arow[off(0)];
-    dre[0] += a0.x * brow[0]; dim[0] += a0.y * brow[4];
-    return;
-#endif
     float2 a[PD];
     float b[PD];
 #pragma unroll

@@ -451,17 +451,3 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
 }
 
 }  // namespace mk
-#ifdef MODEM_STAMPS
-// Diagnostic builds only: copy (and optionally clear) the RX stamp buffer (tools/stamps.py).
-extern "C" int modem_debug_rx_stamps(void* dst, size_t bytes, int clear) {
-    const size_t n = sizeof(mk::g_modem_stamps);
-    if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(mk::g_modem_stamps), bytes < n ? bytes : n, 0,
-                                   hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    if (clear) {
-        void* a = nullptr;
-        if (hipGetSymbolAddress(&a, HIP_SYMBOL(mk::g_modem_stamps)) != hipSuccess) return -2;
-        if (hipMemset(a, 0, n) != hipSuccess) return -3;
-    }
-    return hipDeviceSynchronize() == hipSuccess ? (int)(n / 8) : -4;
-}
-#endif

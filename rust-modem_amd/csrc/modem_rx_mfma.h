@@ -62,23 +62,6 @@ template <> struct InIO<int16_t> {
     }
 };
 
-// Diagnostic builds only (-DMODEM_STAMPS, tools/stamps.py): s_memtime per wave at the phase
-// boundaries of each tile, stored by lane 0 (a vector store) into a buffer nothing else reads.
-// Layout [block * 4 + wave][tile slot 0..7][point 0..7]; tile slot 7 holds the wave's header
-// (entry / exit clocks, HW_ID, XCC_ID).
-#ifdef MODEM_STAMPS
-constexpr int kStampWaves = 8192, kStampTiles = 8, kStampPts = 8;
-static __device__ unsigned long long g_modem_stamps[kStampWaves * kStampTiles * kStampPts];
-__device__ __forceinline__ void modem_stamp(int tile, int pt, unsigned long long v) {
-    const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
-    if ((threadIdx.x & 63) == 0 && w < kStampWaves && tile < kStampTiles)
-        g_modem_stamps[((size_t)w * kStampTiles + tile) * kStampPts + pt] = v;
-}
-#define RX_STAMP(t, k) modem_stamp((int)(t), (k), __builtin_amdgcn_s_memtime())
-#else
-#define RX_STAMP(t, k) ((void)0)
-#endif
-
 enum { MIX_COMPLEX = 0, MIX_REFERENCE_REAL = 1, MIX_REFERENCE_REAL_EXACT = 2 };
 enum { SLICER_NONE = 0, SLICER_NEAREST = 1, SLICER_QAM_AXIS = 2 };
 
@@ -430,12 +413,6 @@ struct RxMfma {
     __device__ static QT load_slot(__amdgpu_buffer_rsrc_t r, int voff, int u) {
         constexpr int S = sizeof(InT) * 2;
         const int o = voff + 4 * NT * u * S;
-#ifdef MODEM_RX_ABLATE_LOAD          // profiling builds only: no sample loads
-        if constexpr (std::is_same<InT, float>::value) {
-            const float v = 0.5f + 0x1p-20f * (float)(o & 1023);
-            return QT{make_float4(v, -v, v, v), make_float4(-v, v, v, -v)};
-        }
-#endif
         if constexpr (std::is_same<InT, float>::value) {
             const f32x4 a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
             const f32x4 b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, o + 16, 0, 0));
@@ -755,9 +732,6 @@ struct RxMfma {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         const float sc = __builtin_ldexpf(1.0f, kpred);
         const cf2 win = window(kpred);
-#ifdef MODEM_STAMPS
-        const int& i = w.i;
-#endif
         while (w.i < w.count) {
             const int64_t t = w.t;
             const bool fi = w.full();
@@ -767,44 +741,18 @@ struct RxMfma {
             // the staging (VALU-bound, the limiting stage) issues ahead of the other
             // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
             // event, +0.8 % bench (profiles/r02_store_layout_ab.txt; priority 3: no better)
-            RX_STAMP(i, 0);
             __builtin_amdgcn_s_setprio(1);
             stage<SC>(p, pl, votes, ix, sc, win, pre, nxt);
-#ifdef MODEM_RX_PAD_SNOP            // sensitivity builds only: extra scalar issue per tile
-#pragma unroll
-            for (int k = 0; k < MODEM_RX_PAD_SNOP; ++k) asm volatile("s_nop 0");
-#endif
-#ifdef MODEM_RX_PAD_VALU            // sensitivity builds only: extra vector issue per tile
-            {
-                float dv = (float)threadIdx.x;
-#pragma unroll
-                for (int k = 0; k < MODEM_RX_PAD_VALU; ++k) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(dv));
-                asm volatile("" :: "v"(dv));
-            }
-#endif
             __builtin_amdgcn_s_setprio(0);
-            RX_STAMP(i, 1);
             __syncthreads();
-            RX_STAMP(i, 2);
             if (!(fi && fast_ok(votes, kpred))) return;
             if (t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
             f32x4 dre, dim;
             if (NWF == NW || wave < NWF) {     // uniform
-#ifdef MODEM_RX_ABLATE_FIR          // profiling builds only: no matched filter
-                dre = (f32x4){1.f, 1.f, 1.f, 1.f}; dim = dre;
-#else
                 fir(pl, tbl, dre, dim);
-#endif
-                RX_STAMP(i, 3);
-#ifdef MODEM_RX_ABLATE_STORE        // profiling builds only: no output stores
-                asm volatile("" :: "v"(dre[0] + dre[1] + dre[2] + dre[3] + dim[0] + dim[1] + dim[2] + dim[3]));
-#else
                 emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
-#endif
-                RX_STAMP(i, 4);
             }
             __syncthreads();                   // the planes are restaged next
-            RX_STAMP(i, 5);
             w.next();
         }
     }
@@ -817,7 +765,6 @@ struct RxMfma {
     __device__ __forceinline__ static void run(const RxParams& p, _Float16* pl, _Float16* tbl, const _Float16* __restrict__ tables,
                                float* red, const TileSeq sq, int64_t bid, const RxHandoff& ho = RxHandoff{}) {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-        RX_STAMP(7, 0);
         const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
         Walk w = walk(p, sq, cx.fast);
         int* votes = reinterpret_cast<int*>(red);            // [4]
@@ -888,35 +835,22 @@ struct RxMfma {
             kpred = read_ka(reds);
             __syncthreads();
         }
-#ifdef MODEM_STAMPS
-        modem_stamp(7, 1, __builtin_amdgcn_s_memrealtime());
-        modem_stamp(7, 2, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
-        modem_stamp(7, 3, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
-        modem_stamp(7, 6, (unsigned long long)sq.first);
-        const int& i = w.i;
-#endif
         while (w.i < w.count) {
             if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
             else loop<true, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
             if (w.i < w.count) {               // tile w.t on the general path (one place in the code)
-                RX_STAMP(i, 6);
                 if constexpr (HO) {            // it reads HBM: this workgroup's sample stores first
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
                 }
                 kpred = slow_tile<EM>(p, pl, tbl, reds, w.t, cx.kb, cx.ld);
                 if (w.t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
-                RX_STAMP(i, 7);
                 w.next();
                 // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
                 // not held across the general path, which has no registers to spare)
                 prefetch(w.q, w.i < w.count && w.full());
             }
         }
-        RX_STAMP(7, 4);
-#ifdef MODEM_STAMPS
-        modem_stamp(7, 5, __builtin_amdgcn_s_memrealtime());
-#endif
     }
 };
 

@@ -44,11 +44,7 @@ __device__ __forceinline__ void tx_emit_off(const TxParams& p, int64_t jb, int o
                                             bool two) {
     const int64_t j = jb + off;
     float2 z0 = y0, z1 = y1;
-#ifdef MODEM_ABLATE_MIX
-    if (false) {
-#else
     if (OUT_MODE != OUT_IQ_BASEBAND) {
-#endif
         const uint64_t nb = p.s0 + (uint64_t)jb;
         float s, c;
         sincos_phase(carrier_phase_off(p.w, nb, off, p.exact_idx), s, c);
@@ -162,10 +158,6 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
 #pragma unroll
         for (int r = 0; r < R; ++r) win[r] = ldc(base + r);
         int k = 0;
-#ifdef MODEM_ABLATE_FIR
-        k = K;
-        acc[0][0] = win[0];
-#endif
         for (; k + CH <= K; k += CH) {
             const float2* pc = base - (k + CH);   // positive ds_read immediates: pc[CH-1-c]
 #pragma unroll
@@ -531,17 +523,3 @@ hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStr
 
 }  // namespace mk
 
-#ifdef MODEM_STAMPS
-// Diagnostic builds only: copy (and optionally clear) the TX stamp buffer (tools/stamps.py).
-extern "C" int modem_debug_tx_stamps(void* dst, size_t bytes, int clear) {
-    const size_t n = sizeof(mk::g_modem_tx_stamps);
-    if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(mk::g_modem_tx_stamps), bytes < n ? bytes : n, 0,
-                                   hipMemcpyDeviceToHost) != hipSuccess) return -1;
-    if (clear) {
-        void* a = nullptr;
-        if (hipGetSymbolAddress(&a, HIP_SYMBOL(mk::g_modem_tx_stamps)) != hipSuccess) return -2;
-        if (hipMemset(a, 0, n) != hipSuccess) return -3;
-    }
-    return hipDeviceSynchronize() == hipSuccess ? (int)(n / 8) : -4;
-}
-#endif

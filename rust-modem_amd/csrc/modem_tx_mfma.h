@@ -6,23 +6,6 @@
 
 namespace mk {
 
-// Diagnostic builds only (-DMODEM_STAMPS, tools/stamps.py --kernel tx): s_memtime per wave at the
-// phase boundaries of each TX tile (lane 0's vector store into a buffer nothing else reads).
-// Layout [block * 4 + wave][tile slot 0..7][point 0..7]; slot 7: entry / realtime / HW_ID / XCC_ID
-// / exit / realtime.
-#ifdef MODEM_STAMPS
-constexpr int kTxStampWaves = 8192, kTxStampTiles = 8, kTxStampPts = 8;
-static __device__ unsigned long long g_modem_tx_stamps[kTxStampWaves * kTxStampTiles * kTxStampPts];
-__device__ __forceinline__ void modem_tx_stamp(int tile, int pt, unsigned long long v) {
-    const int w = (int)blockIdx.x * 4 + ((int)threadIdx.x >> 6);
-    if ((threadIdx.x & 63) == 0 && w < kTxStampWaves && tile < kTxStampTiles)
-        g_modem_tx_stamps[((size_t)w * kTxStampTiles + tile) * kTxStampPts + pt] = v;
-}
-#define TX_STAMP(t, k) modem_tx_stamp((int)(t), (k), __builtin_amdgcn_s_memtime())
-#else
-#define TX_STAMP(t, k) ((void)0)
-#endif
-
 // ---------------------------------------------------------------- symbol mapping (TX) ----
 // bytes_to_bits (digital/util.rs:5-11) of symbol m's bits, MSB first, `b & 1` per byte.
 __device__ __forceinline__ uint32_t tx_symbol_index(const TxParams& p, int64_t m) {
@@ -230,12 +213,6 @@ struct TxMfma {
             const tq4 x = *reinterpret_cast<const tq4*>(a), y = *reinterpret_cast<const tq4*>(a + 4);
             return (th8){x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
         };
-#ifdef MODEM_ABLATE_FIR
-        const th8 a0 = ld8(ar);
-        dre = (f32x4){(float)a0[0], 0.f, 0.f, 0.f};
-        dim = (f32x4){(float)bh[0][0], 0.f, 0.f, 0.f};
-        return;
-#endif
         f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;     // one accumulator per rail
         th8 a[2][4];
         auto load = [&](int s, int slot) {
@@ -280,7 +257,6 @@ struct TxMfma {
 #pragma unroll
             for (int r = 0; r < 4; ++r) z[r] *= unscale;
         }
-#ifndef MODEM_ABLATE_MIX
         if (OUT_MODE != OUT_IQ_BASEBAND) {
             // rows (0, 1) and (2, 3) as two packed phase pairs, side by side
             const cf2 nf0 = (cf2){idx_f32(nb), idx_f32(nb + 16.0)};
@@ -294,7 +270,6 @@ struct TxMfma {
             z[2] = tx_cmix(z[2], (cf2){cs1.x, sn1.x});
             z[3] = tx_cmix(z[3], (cf2){cs1.y, sn1.y});
         }
-#endif
         if constexpr (RAW) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -302,10 +277,6 @@ struct TxMfma {
                 if (i >= 0 && i < ro.n) ro.p[i] = make_float2(z[r].x, z[r].y);
             }
         }
-#ifdef MODEM_ABLATE_STORE
-#pragma unroll
-        for (int r = 0; r < 4; ++r) asm volatile("" :: "v"(z[r]));
-#else
         // wave-uniform base in SGPRs + 32-bit lane byte offsets (saddr + voffset stores)
         constexpr int SBYTES = (OUT_MODE == OUT_REAL ? 1 : 2) * (int)sizeof(OutT);
         const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
@@ -323,7 +294,6 @@ struct TxMfma {
                 else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
             }
         }
-#endif
     }
 
     // Partial tile, samples before the call, or carrier index >= 2^53: guarded, 64-bit
@@ -483,39 +453,23 @@ struct TxMfma {
         int64_t t = t0;
         // the first tile's bits are requested before the LUT goes to LDS, so that the two
         // memory latencies at the kernel's start overlap
-        TX_STAMP(7, 0);
         bool ready = t < t1 && full(t);
         if (ready) prefetch(t);
         const th4* lut_h = reinterpret_cast<const th4*>(p.lut_h);
         for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = lut_h[i];
         __syncthreads();   // LUT visible
         if (xs > 0 && t0 > 0) tail(p, pl, lut_s, bh, bl, t0 - 1, xs, unscale);
-#ifdef MODEM_STAMPS
-        modem_tx_stamp(7, 1, __builtin_amdgcn_s_memrealtime());
-        modem_tx_stamp(7, 2, __builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
-        modem_tx_stamp(7, 3, __builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
-        int si = 0;
-#endif
         while (t < t1) {
             if (full(t)) {
                 if (!ready) prefetch(t);
                 ready = false;
                 for (; t < t1 && full(t); t += ts) {
-#ifdef MODEM_STAMPS
-                    TX_STAMP(si, 0);
-#endif
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const int e = tid + NT * u;
                         if (e < NE) put(pl, e, lut_s[word_index(pre[u], BPS)]);
                     }
-#ifdef MODEM_STAMPS
-                    TX_STAMP(si, 1);
-#endif
                     __syncthreads();
-#ifdef MODEM_STAMPS
-                    TX_STAMP(si, 2);
-#endif
                     if (t + ts < t1) prefetch(t + ts);   // next bits fly during the MFMAs
                     const int64_t j0 = (t * TS - lead) * SPS;
 #pragma unroll
@@ -530,19 +484,9 @@ struct TxMfma {
                         emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                         __builtin_amdgcn_s_setprio(0);
                     }
-#ifdef MODEM_STAMPS
-                    TX_STAMP(si, 4);
-#endif
                     __syncthreads();                     // the window is restaged next trip
-#ifdef MODEM_STAMPS
-                    TX_STAMP(si, 5);
-                    ++si;
-#endif
                 }
             } else {
-#ifdef MODEM_STAMPS
-                TX_STAMP(si, 6);
-#endif
                 stage_slow(p, pl, lut_s, t * TS - lead - PRE);
                 __syncthreads();
                 const int64_t j0 = (t * TS - lead) * SPS;
@@ -554,17 +498,9 @@ struct TxMfma {
                     emit_edge(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                 }
                 __syncthreads();
-#ifdef MODEM_STAMPS
-                TX_STAMP(si, 7);
-                ++si;
-#endif
                 t += ts;
             }
         }
-        TX_STAMP(7, 4);
-#ifdef MODEM_STAMPS
-        modem_tx_stamp(7, 5, __builtin_amdgcn_s_memrealtime());
-#endif
     }
 };
 

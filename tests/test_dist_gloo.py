@@ -140,12 +140,14 @@ def test_gpus_flag_spawns_ranks(monkeypatch):
         def __init__(self, cmd, env, stdout, text):
             started.append((cmd, {k: env[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}))
             self.rank = int(env["RANK"])
+            if self.rank == 0:
+                stdout.write("log line\n" + json.dumps({"n_gpus": 4, "value": 1.0}) + "\n")
+                stdout.flush()
 
-        def communicate(self):
-            line = json.dumps({"n_gpus": 4, "value": 1.0}) if self.rank == 0 else ""
-            return ("log line\n" + line + "\n", None)
+        def poll(self):
+            return 0
 
-        def wait(self):
+        def wait(self, timeout=None):
             return 0
 
     monkeypatch.setattr(subprocess, "Popen", FakePopen)
@@ -194,3 +196,26 @@ def test_settle_clocks_runs_untimed_steps_for_the_budget():
     assert out["steps"] == r.steps and r.steps >= 20
     assert 60.0 <= out["ms"] <= dt + 1.0 and dt < 60.0 + 20.0     # batches end near the budget
     assert r.syncs < r.steps                                      # steps are queued in batches
+
+
+def test_spawn_ends_ranks_when_one_fails():
+    """bench._wait_ranks polls every rank: a rank that exits non-zero ends the others (a rank
+    waiting in a barrier for a dead peer would otherwise hang the bench) and its code is the
+    one reported; an overall timeout ends every rank with 124."""
+    import subprocess
+    import sys
+    import bench
+    sleeper = [sys.executable, "-c", "import time; time.sleep(60)"]
+    procs = [subprocess.Popen(sleeper), subprocess.Popen([sys.executable, "-c", "raise SystemExit(3)"]),
+             subprocess.Popen(sleeper)]
+    t0 = time.monotonic()
+    rcs, first_bad = bench._wait_ranks(procs, timeout_s=50)
+    assert time.monotonic() - t0 < 30
+    assert first_bad == 3 and rcs[1] == 3
+    assert all(p.poll() is not None for p in procs)
+    procs = [subprocess.Popen(sleeper) for _ in range(2)]
+    t0 = time.monotonic()
+    rcs, first_bad = bench._wait_ranks(procs, timeout_s=1.0)
+    assert time.monotonic() - t0 < 30
+    assert first_bad == 124 and rcs == [124, 124]
+    assert all(p.poll() is not None for p in procs)

@@ -105,3 +105,51 @@ def test_fused_chain_equals_two_launches(m, o, torch_cuda, cfg, dtype, nsym, ext
     k0 = max(0, -(-(c_prev - (L - 1)) // sps))             # its first kept instant
     got = bufs[0][2][:k1].cpu().numpy()
     assert nsym_p > 0 and np.array_equal(got, sent[k0: k0 + k1]), "decisions are not the symbols sent"
+
+
+# the fused forms also exist with one RX output only (RXE_IQ: I/Q, no slicer output; RXE_SYM:
+# decisions only): (config, dtype, symbols per period, periods, form expected after period 0)
+ONE_OUTPUT_CASES = [
+    ("c2_qpsk", 0, 1 << 18, 3, 2),      # chain_small: the LDS hand-off form
+    ("c5_qam256", 0, 1 << 17, 3, 1),    # chain_mfma: the drained-stores form
+]
+
+
+@pytest.mark.parametrize("which", ["iq", "sym"])
+@pytest.mark.parametrize("cfg,dtype,nsym,periods,form", ONE_OUTPUT_CASES)
+def test_fused_chain_one_output(m, o, torch_cuda, cfg, dtype, nsym, periods, form, which):
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS[cfg]
+    nb = nsym * bps
+    hb = o.prng_bits(SEED + 77 + nsym % 1000, nb)
+    bits = torch.from_numpy(hb).cuda()
+    tdt = torch.float16 if dtype else torch.float32
+    cap = nb // bps * sps
+    bufs = []
+    for _ in range(2):
+        y = torch.empty((cap, 2), dtype=tdt, device="cuda")
+        q = torch.empty((cap // sps + 1, 2), dtype=tdt, device="cuda") if which == "iq" else None
+        s = torch.empty(cap // sps + 1, dtype=torch.uint8, device="cuda") if which == "sym" else None
+        bufs.append((y, q, s))
+    (txf, rxf), (txt, rxt) = make_pair(m, o, cfg, dtype, 1.0), make_pair(m, o, cfg, dtype, 1.0)
+    fused = m.ChainPlan(txf, rxf, bits, *bufs[0])
+    os.environ["MODEM_CHAIN_FUSED"] = "0"
+    try:
+        two = m.ChainPlan(txt, rxt, bits, *bufs[1])
+    finally:
+        del os.environ["MODEM_CHAIN_FUSED"]
+    how = []
+    for p in range(periods):
+        n1, k1 = fused.run()
+        n2, k2 = two.run()
+        torch.cuda.synchronize()
+        assert (n1, k1) == (n2, k2), p
+        how.append(fused.fused)
+        (y1, q1, s1), (y2, q2, s2) = bufs
+        assert torch.equal(y1[:n1], y2[:n2]), f"period {p}: samples differ"
+        if which == "iq":
+            assert torch.equal(q1[:k1], q2[:k2]), f"period {p}: RX I/Q differ"
+        else:
+            assert torch.equal(s1[:k1], s2[:k2]), f"period {p}: decisions differ"
+    assert all(h == form for h in how[1:]), how
+    print(f"\n[fused one output] {cfg} {which}: forms {how}")
