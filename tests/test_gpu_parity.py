@@ -431,6 +431,31 @@ def test_c_host_loopback():
     assert "0 wrong" in r.stdout
 
 
+@pytest.mark.parametrize("src", ["bits", "evenodd", "ascii"])
+def test_rust_source_binding(o, tmp_path, src):
+    """tests/cpp/rust_source.c: the Rust binding's Source-driven HipModulator
+    restated in C — the handle created from the Rust TxDesc layout (q_offset = sps / 2 for the
+    EvenOddOffset source), the bits gathered from data.rs's Bits / EvenOddOffset / AsciiBits state
+    machines at their Changed events, chunked modem_tx_process calls — against the oracle's
+    DigitalModulator over the same source (`modulate --iq` of qpsk and oqpsk), bit for bit."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    exe = os.path.join(ROOT, "tests", "cpp", "rust_source")
+    assert os.path.exists(exe), "tests/cpp/rust_source not built (build())"
+    out = str(tmp_path / "y.f32")
+    r = subprocess.run([exe, src, out], capture_output=True, text=True, timeout=90)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0
+    got = np.fromfile(out, dtype=np.float32).reshape(-1, 2)
+    bits = np.fromfile(out + ".bits", dtype=np.uint8)
+    eo = src == "evenodd"
+    ph = o.new_phasor(o.OQPSK, 1.0) if eo else o.new_phasor(o.QPSK, 0.0, 1.0)
+    ref = o.tx_chain(ph, bits, 8, None, o.sample_freq(1000, 10000), 0, out_mode=o.OUT_IQ_BASEBAND, even_odd=eo)
+    assert got.shape == ref.shape == ((len(bits) // 2) * 8, 2)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
 @pytest.mark.parametrize("cfg,dtype", [("c3_qam16", 0), ("c2_qpsk", 0), ("c5_qam256", 1)])
 def test_chain_plan_equals_separate_calls(m, o, torch_cuda, cfg, dtype):
     """modem_chain_run (ChainPlan: the bench's step) equals modem_tx_process followed by
