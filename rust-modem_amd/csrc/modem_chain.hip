@@ -78,7 +78,7 @@ void chain_mfma(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
     if (bid == nb - 1) rx_state_update<T>(rp);
     // ---- RX: tiles r1 - 1 down to r0 (the last written first)
     _Float16* pl = lds_c;
-    _Float16* tbl = lds_c + 4 * RK::PL;
+    _Float16* tbl = lds_c + RK::TBL_OFF;
     float* red = reinterpret_cast<float*>(tbl + RK::NC * 2 * RK::TB);
     const TileSeq sq{r1 - 1, -1, r1 - r0, g.nrx};
     RK::template run<EM>(rp, pl, tbl, tables, red, sq, bid);
@@ -95,7 +95,7 @@ struct SmallLds {
     using TK = TxMfma<SPS, NKS_T, OUT_IQ_MIXED, float, 1>;
     using RK = RxMfma<SPS, NKS_R, float, MIX_COMPLEX, float, 1>;
     static constexpr int TXH = 2 * TK::PLANES + 256 * 4;                 // + the largest LUT
-    static constexpr int A = ((TXH > 4 * RK::PL ? TXH : 4 * RK::PL) + 7) & ~7;
+    static constexpr int A = ((TXH > RK::TBL_OFF ? TXH : RK::TBL_OFF) + 7) & ~7;
     static constexpr int TBL = A, RED = A + RK::NC * 2 * RK::TB, RAW = (RED + 16 + 7) & ~7;
     static size_t bytes(int raw_n) { return (size_t)(RAW + 4 * raw_n) * 2; }
 };

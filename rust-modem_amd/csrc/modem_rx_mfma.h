@@ -324,17 +324,31 @@ struct RxMfma {
     static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
     static constexpr int NQ = (NS + 3) / 4;                     // quads
     static constexpr int U = (NQ + NT - 1) / NT;                // quads per lane
-    // Plane layout. decim 4: unpadded, 16-B chunks XOR-swizzled within each aligned group of
-    // 8 chunks — conflict-free A reads (tests/test_lds_banks.py) and 4 KiB less LDS per
-    // workgroup than padding, which lets 4 workgroups share a CU. Otherwise rxh_pos.
-    static constexpr bool SWZ = DEC == 4 && NT == 256;
+    // Plane layout. decim 4 and 8: unpadded, 16-B chunks XOR-swizzled within each row of
+    // 8 (decim 4) or 16 (decim 8) chunks by the row bits — conflict-free A reads and staging
+    // writes (tests/test_lds_banks.py) and no pad halves, which lets 4 workgroups share a CU
+    // (decim 4; decim 8 with two planes). Otherwise rxh_pos.
+    static constexpr bool SWZ = (DEC == 4 || DEC == 8) && NT == 256;
     __host__ __device__ static constexpr int ppos(int e) {
-        return SWZ ? ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7)) : rxh_pos(e, RW);
+        return !SWZ ? rxh_pos(e, RW)
+             : DEC == 4 ? ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7))
+                        : ((((e >> 3) ^ (((e >> 7) & 7) << 1)) << 3) | (e & 7));
     }
     static constexpr int PL = SWZ ? (4 * NQ + 63) & ~63 : (rxh_pos(4 * NQ - 1, RW) + 1 + 7) & ~7;   // halves per plane
+    // f16 samples in and out (the f16 storage sweep, SURVEY.md §8c tolerance 2^-10): the mixed
+    // samples are staged as their f16 roundings only (two planes, re and im; the f32 path's
+    // lo planes carry bits below the f16 output's precision: +2^-12.4 of max|y| before the
+    // output rounding on C5, tests/test_gpu_range.py), 2 MFMAs per rail and k-step instead of
+    // 3, and half the LDS: C5 f16 fits 4 workgroups per CU instead of 2. Otherwise four planes
+    // (re_hi, re_lo, im_hi, im_lo).
+    static constexpr bool HI = std::is_same<InT, __half>::value && std::is_same<OutT, __half>::value;
+    static constexpr int NPL = HI ? 2 : 4;
     static constexpr int NC = rx_mfma_table_copies(DEC);
     static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
-    static constexpr size_t LDS_BYTES = (size_t)4 * PL * 2 + (size_t)NC * 2 * TB * 2 + 8 * 4;   // + votes, maxima
+    // the planes, whose LDS the general path also uses for the raw window (NS float2, or NS
+    // half2 for f16 input with HI: within NPL * PL halves either way), the tap tables, votes
+    static constexpr int TBL_OFF = NPL * PL;                    // halves
+    static constexpr size_t LDS_BYTES = (size_t)TBL_OFF * 2 + (size_t)NC * 2 * TB * 2 + 8 * 4;   // + votes, maxima
     static constexpr int K_TAB8 = NC * 2 * TB / 8;              // 16-B chunks of the tap tables
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
     // Waves per SIMD the registers are held to: 4 where the LDS lets 4 workgroups share a CU
@@ -440,9 +454,13 @@ struct RxMfma {
         auto load = [&](int s, int c) {
             const _Float16* ap = pl + ppos(ae + 32 * s);
             a[c][0] = *reinterpret_cast<const h8*>(ap);
-            a[c][1] = *reinterpret_cast<const h8*>(ap + PL);
-            a[c][2] = *reinterpret_cast<const h8*>(ap + 2 * PL);
-            a[c][3] = *reinterpret_cast<const h8*>(ap + 3 * PL);
+            if (HI) {
+                a[c][2] = *reinterpret_cast<const h8*>(ap + PL);
+            } else {
+                a[c][1] = *reinterpret_cast<const h8*>(ap + PL);
+                a[c][2] = *reinterpret_cast<const h8*>(ap + 2 * PL);
+                a[c][3] = *reinterpret_cast<const h8*>(ap + 3 * PL);
+            }
             b[c][0] = *reinterpret_cast<const h8*>(brow + 32 * s);
             b[c][1] = *reinterpret_cast<const h8*>(brow + TB + 32 * s);
         };
@@ -456,16 +474,25 @@ struct RxMfma {
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][1], m0, 0, 0, 0);
-            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], b[c][0], r0, 0, 0, 0);
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], b[c][0], m0, 0, 0, 0);
+            if (!HI) {
+                r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], b[c][0], r0, 0, 0, 0);
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], b[c][0], m0, 0, 0, 0);
+            }
             __builtin_amdgcn_sched_barrier(0);
         }
         dre = r0;
         dim = m0;
     }
 
-    // Split z (4 samples) and write it at plane offset o.
+    // Split z (4 samples) and write it at plane offset o (HI: the f16 roundings only).
     __device__ static void put4(_Float16* pl, int o, const float (&zr)[4], const float (&zi)[4]) {
+        if constexpr (HI) {
+            const h2 r0 = __builtin_convertvector((cf2){zr[0], zr[1]}, h2), r1 = __builtin_convertvector((cf2){zr[2], zr[3]}, h2);
+            const h2 i0 = __builtin_convertvector((cf2){zi[0], zi[1]}, h2), i1 = __builtin_convertvector((cf2){zi[2], zi[3]}, h2);
+            *reinterpret_cast<h4*>(pl + o) = (h4){r0.x, r0.y, r1.x, r1.y};
+            *reinterpret_cast<h4*>(pl + PL + o) = (h4){i0.x, i0.y, i1.x, i1.y};
+            return;
+        }
         h2 rh0, rl0, rh1, rl1, ih0, il0, ih1, il1;
         split2((cf2){zr[0], zr[1]}, rh0, rl0);
         split2((cf2){zr[2], zr[3]}, rh1, rl1);
@@ -595,7 +622,10 @@ struct RxMfma {
         //    first tile took 10-16 us against ~3.5 for a fast one (r03 stamps, tools/stamps.py).
         //    The window's samples before the chunk (only a call's first tile has them) are then
         //    patched in from the history.
-        float2* raw = reinterpret_cast<float2*>(pl);
+        // raw window: float2, or the exact half2 inputs when HI (it must fit the two planes)
+        using RawT = typename std::conditional<HI, __half2, float2>::type;
+        RawT* raw = reinterpret_cast<RawT*>(pl);
+        static_assert((size_t)NS * sizeof(RawT) <= (size_t)NPL * PL * 2, "raw window within the planes' LDS");
         {
             constexpr int S = sizeof(InT) * 2;
             constexpr int NK = (NS + NT - 1) / NT, BATCH = 8;
@@ -605,15 +635,17 @@ struct RxMfma {
             const __amdgpu_buffer_rsrc_t rx = buf_rsrc(reinterpret_cast<const char*>(p.x) + qx * S,
                                                        (uint32_t)(nx > 0 ? nx : 0) * S);
             const int ox = (int)ex;
-            auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+            auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) -> RawT {
                 if constexpr (std::is_same<InT, float>::value)
                     return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+                else if constexpr (HI)
+                    return __builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
                 else
                     return __half22float2(__builtin_bit_cast(__half2, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0)));
             };
 #pragma unroll
             for (int k0 = 0; k0 < NK; k0 += BATCH) {
-                float2 v[BATCH];
+                RawT v[BATCH];
 #pragma unroll
                 for (int b = 0; b < BATCH; ++b)       // < 0: wraps, out of range -> 0
                     if (k0 + b < NK) v[b] = ld(rx, (uint32_t)(tid + (k0 + b) * NT - ox) * S);
@@ -633,7 +665,7 @@ struct RxMfma {
                 const int oh = (int)eh;
                 for (int k = 0; k * NT < ox && k < NK; ++k) {         // uniform bounds
                     const int e = tid + k * NT;
-                    const float2 w = ld(rh, (uint32_t)(e - oh) * S);
+                    const RawT w = ld(rh, (uint32_t)(e - oh) * S);
                     if (e < ox && e < NS) raw[e] = w;
                 }
             }
@@ -648,7 +680,10 @@ struct RxMfma {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 float2 z = make_float2(0.f, 0.f);
-                if (e0 + j < NS) z = rx_mix<MIX>(p, n_lo, e0 + j, raw[e0 + j]);
+                if (e0 + j < NS) {
+                    if constexpr (HI) z = rx_mix<MIX>(p, n_lo, e0 + j, __half22float2(raw[e0 + j]));
+                    else z = rx_mix<MIX>(p, n_lo, e0 + j, raw[e0 + j]);
+                }
                 zr[u][j] = z.x;
                 zi[u][j] = z.y;
                 mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(z.x), __builtin_fabsf(z.y)));
@@ -862,7 +897,7 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
     _Float16* pl = lds_h;                                   // 4 sample planes
-    _Float16* tbl = lds_h + 4 * K::PL;                      // NC x (hi, lo) tap tables
+    _Float16* tbl = lds_h + K::TBL_OFF;                     // NC x (hi, lo) tap tables
     float* red = reinterpret_cast<float*>(tbl + K::NC * 2 * K::TB);
     if (bid == 0) rx_state_update<InT>(p);
     const int64_t ntiles = (p.nout + K::lead(p) + K::TS - 1) / K::TS;

@@ -93,6 +93,37 @@ def swz_pos(e):
     return ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7))
 
 
+def swz8_pos(e):
+    """RxMfma::ppos for decim 8 (4 waves): 16-B chunks XOR-swizzled within each 128-sample
+    row of 16 chunks by the row's low 3 bits."""
+    return ((((e >> 3) ^ (((e >> 7) & 7) << 1)) << 3) | (e & 7))
+
+
+def test_swizzled_decim8_layout_conflict_free():
+    """C5's RX (decim 8, 20 k-steps; two planes for f16 samples, four for f32): the unpadded
+    swizzled plane. A reads: lane (i, g) of wave w, k-step s reads 8 halves at sample
+    (16 w + i) * 128 + 8 g + 32 s; staging writes: ds_write_b64 of 4 consecutive samples per
+    lane, slots 1024 samples apart; the swizzle is a bijection within every row (no LDS
+    beyond the unpadded plane) and repeats every 1024 samples (the slot offset)."""
+    for w in range(4):
+        for s in range(20):
+            assert extra_cycles(lambda l: 2 * swz8_pos((16 * w + (l & 15)) * 128 + 8 * (l >> 4) + 32 * s)) == 0
+    for u in range(9):
+        for g in range(4):
+            banks = {}
+            for lane in range(16 * g, 16 * g + 16):
+                a = 2 * swz8_pos(4 * lane + 1024 * u)
+                for d in range(2):
+                    banks.setdefault((a // 4 + d) % 32, set()).add(a)
+            assert max(len(v) for v in banks.values()) == 1
+    for base in range(0, 8192, 128):
+        assert sorted(swz8_pos(e) for e in range(base, base + 128)) == list(range(base, base + 128))
+    for e in range(0, 4096):
+        assert swz8_pos(e + 1024) == swz8_pos(e) + 1024
+    # the unswizzled, unpadded decim-8 plane would be 15-way conflicted on every A read
+    assert extra_cycles(lambda l: 2 * ((l & 15) * 128 + 8 * (l >> 4))) > 0
+
+
 def test_swizzled_layout_conflict_free():
     # A reads: lane (i, g) of wave w, k-step s reads 8 halves at sample (16 w + i) * 64 + 8 g + 32 s
     for w in range(4):

@@ -68,6 +68,32 @@ __global__ __launch_bounds__(256) void k_fused(const uint4* bits, float4* y, flo
     __syncthreads();
     if (t - G < NT) rx_tile(y, iq, sym, t - G);
 }
+// lag 0: RX tile t right after TX tile t in the same workgroup (the tile just written)
+__global__ __launch_bounds__(256) void k_fused0(const uint4* bits, float4* y, float4* iq, unsigned* sym) {
+    for (int t = blockIdx.x; t < NT; t += gridDim.x) {
+        tx_tile(bits, y, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        rx_tile(y, iq, sym, t);
+    }
+}
+// the same with the TX tile stored write-through (sc1: the line leaves the XCD's L2)
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void k_fused0_sc1(const uint4* bits, float4* y, float4* iq, unsigned* sym) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(y, 0, 0x7fffffff, 0x00020000);
+    for (int t = blockIdx.x; t < NT; t += gridDim.x) {
+        const uint4 b = bits[(size_t)t * 256 + threadIdx.x];
+        const float v = (float)(b.x ^ b.y ^ b.z ^ b.w);
+        const unsigned base = (unsigned)t * (TS * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128((u4v){__float_as_uint(v), __float_as_uint(v + j), __float_as_uint(v),
+                                                   __float_as_uint(v - j)}, r, base + (j * 256 + threadIdx.x) * 16, 0, 16);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        rx_tile(y, iq, sym, t);
+    }
+}
 __global__ void k_wr(float4* o, size_t n) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         o[i] = make_float4(1, 2, 3, 4);
@@ -80,7 +106,9 @@ __global__ void k_rd(const float4* x, float* o, size_t n) {
     if (a.x == 12345.f) o[0] = a.y + a.z + a.w;
 }
 
+static bool g_quick = false;                     // argv[1] == "pmc": 3 launches each, untimed
 template <typename F> static void run(const char* name, double bytes, F f) {
+    if (g_quick) { for (int i = 0; i < 3; ++i) f(); (void)hipDeviceSynchronize(); printf("%s\n", name); return; }
     for (int i = 0; i < 200; ++i) f();           // settle the clocks
     (void)hipDeviceSynchronize();
     hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
@@ -98,7 +126,8 @@ template <typename F> static void run(const char* name, double bytes, F f) {
     fflush(stdout);
 }
 
-int main() {
+int main(int argc, char** argv) {
+    g_quick = argc > 1 && argv[1][0] == 'p';
     uint4* bits; float4 *y, *iq; unsigned* sym; float* o;
     (void)hipMalloc(&bits, (size_t)NS); (void)hipMalloc(&y, (size_t)NS * 8);
     (void)hipMalloc(&iq, (size_t)NS / 4 * 8); (void)hipMalloc(&sym, (size_t)NS / 4); (void)hipMalloc(&o, 64);
@@ -114,6 +143,10 @@ int main() {
                           hipLaunchKernelGGL(k_rx, G, 256, 0, 0, y, iq, sym); });
         snprintf(n, 96, "fused (tx t, rx t-G) grid %d", G);
         run(n, bch, [&] { hipLaunchKernelGGL(k_fused, G, 256, 0, 0, bits, y, iq, sym); });
+        snprintf(n, 96, "fused lag 0 (tx t, rx t) grid %d", G);
+        run(n, bch, [&] { hipLaunchKernelGGL(k_fused0, G, 256, 0, 0, bits, y, iq, sym); });
+        snprintf(n, 96, "fused lag 0, tx sc1 stores grid %d", G);
+        run(n, bch, [&] { hipLaunchKernelGGL(k_fused0_sc1, G, 256, 0, 0, bits, y, iq, sym); });
         snprintf(n, 96, "tx alone grid %d", G);
         run(n, btx, [&] { hipLaunchKernelGGL(k_tx, G, 256, 0, 0, bits, y); });
         snprintf(n, 96, "rx alone grid %d", G);
