@@ -346,8 +346,8 @@ struct TxMfma {
     // One tile t and, before it, the last xs sub-tiles of tile t - 1 (the fused small call,
     // modem_chain.hip: one RX tile per workgroup). The tail's symbol loads fly with the tile's
     // and the LUT's, both are staged before one barrier (the tail into the second plane set
-    // pl2), and every emitted sample is also written to the LDS window `ro`.
-    template <int BPS>
+    // pl2), and (RAW) every emitted sample is also written to the LDS window `ro`.
+    template <int BPS, bool RAW = true>
     __device__ __forceinline__ static void one_tile(const TxParams& p, _Float16* pl, _Float16* pl2, th4* lut_s,
                                                     const th8 (&bh)[NKS], const th8 (&bl)[NKS], int64_t t, int xs,
                                                     const RawOut& ro) {
@@ -413,12 +413,14 @@ struct TxMfma {
             if (tl && g >= g0) {                                    // wave-uniform
                 if (lv) fir<true>(pl2, q, bh, bl, dre, dim);
                 else fir<false>(pl2, q, bh, bl, dre, dim);
-                emit_edge<true>(p, j2 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
+                emit_edge<RAW>(p, j2 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
             }
             if (lv) fir<true>(pl, q, bh, bl, dre, dim);
             else fir<false>(pl, q, bh, bl, dre, dim);
-            if (fullt) emit_full<true>(p, j0 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
-            else emit_edge<true>(p, j0 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
+            if (!RAW) __builtin_amdgcn_s_setprio(1);                // as run(): the epilogue issues first
+            if (fullt) emit_full<RAW>(p, j0 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
+            else emit_edge<RAW>(p, j0 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
+            if (!RAW) __builtin_amdgcn_s_setprio(0);
         }
         __syncthreads();                                            // the planes are restaged next
     }
