@@ -108,16 +108,21 @@ def test_fused_chain_equals_two_launches(m, o, torch_cuda, cfg, dtype, nsym, ext
 
 
 # the fused forms also exist with one RX output only (RXE_IQ: I/Q, no slicer output; RXE_SYM:
-# decisions only): (config, dtype, symbols per period, periods, form expected after period 0)
+# QAM-axis decisions only): (config, dtype, symbols per period, periods, which output, form
+# expected after period 0). QPSK's nearest-point decisions alone have no steady-state epilogue
+# (rx_mfma_em: RXE_GEN), so that call takes the two launches.
 ONE_OUTPUT_CASES = [
-    ("c2_qpsk", 0, 1 << 18, 3, 2),      # chain_small: the LDS hand-off form
-    ("c5_qam256", 0, 1 << 17, 3, 1),    # chain_mfma: the drained-stores form
+    ("c2_qpsk", 0, 1 << 18, 3, "iq", 2),       # chain_small: the LDS hand-off form
+    ("c2_qpsk", 0, 1 << 18, 3, "sym", 0),      # nearest-point decisions only: two launches
+    ("c3_qam16", 0, 1 << 16, 3, "iq", 2),
+    ("c3_qam16", 0, 1 << 16, 3, "sym", 2),
+    ("c5_qam256", 0, 1 << 17, 3, "iq", 1),     # chain_mfma: the drained-stores form
+    ("c5_qam256", 0, 1 << 17, 3, "sym", 1),
 ]
 
 
-@pytest.mark.parametrize("which", ["iq", "sym"])
-@pytest.mark.parametrize("cfg,dtype,nsym,periods,form", ONE_OUTPUT_CASES)
-def test_fused_chain_one_output(m, o, torch_cuda, cfg, dtype, nsym, periods, form, which):
+@pytest.mark.parametrize("cfg,dtype,nsym,periods,which,form", ONE_OUTPUT_CASES)
+def test_fused_chain_one_output(m, o, torch_cuda, cfg, dtype, nsym, periods, which, form):
     torch = torch_cuda
     name, bps, L, sps = CONFIGS[cfg]
     nb = nsym * bps

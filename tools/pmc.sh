@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes over tools/prof_kernels.py (one counter group per rocprofv3 run; --pmc is never
-# combined with tracing domains). Usage: tools/pmc.sh <outdir> [config]
-out=${1:-gpurun_out/pmc}; cfg=${2:-c3}
+# combined with tracing domains). Usage: tools/pmc.sh <outdir> [config] [prof_kernels args...]
+out=${1:-gpurun_out/pmc}; cfg=${2:-c3}; shift $(( $# < 2 ? $# : 2 )); extra="$@"
 export TMPDIR=/tmp
 mkdir -p "$out"
 groups=(
@@ -16,7 +16,7 @@ groups=(
 i=0
 for g in "${groups[@]}"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $g --output-format csv -d "$out/p$i" -o run -- python3 tools/prof_kernels.py --config $cfg --reps 10 > "$out/p$i.log" 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $g --output-format csv -d "$out/p$i" -o run -- python3 tools/prof_kernels.py --config $cfg --reps 10 $extra > "$out/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc ($g)"
   case $rc in 124|134|137|139) echo "stopping after rc=$rc"; exit $rc;; esac

@@ -8,7 +8,8 @@ from collections import defaultdict
 
 
 def short(name):
-    for key in ("tx_fast", "rx_fast", "tx_mfma", "rx_mfma", "tx_generic", "rx_generic", "fir_real", "prng_bits"):
+    for key in ("tx_fast", "rx_fast", "tx_mfma", "rx_mfma", "tx_generic", "rx_generic", "fir_real", "prng_bits",
+                "chain_small", "chain_mfma", "chain_flow"):
         if key in name:
             return name.split("(")[0].replace("void mk::", "")
     return None
