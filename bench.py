@@ -532,7 +532,7 @@ def out_of_cache_roofline(runner_factory, config="c5"):
     t_tx, t_rx, t_chain = r.kernel_times_ms(10, rounds=3)
     b_tx, b_rx, _ = algorithmic_bytes(bps, L, sps, nsamp, dtype)
     rx_gbs = b_rx / (t_rx * 1e-3) / 1e9
-    chain_gbs = b_moved / (t_chain * 1e-3) / 1e9
+    chain_gbs = (b_tx + b_rx) / (t_chain * 1e-3) / 1e9
     return {"workload": desc, "kernel": "rx", "achieved": round(rx_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(rx_gbs / HBM_PEAK_GBS, 4), "mean_launch_ms": round(t_rx, 5),
             "algorithmic_bytes_per_launch": b_rx, "tx_ms": round(t_tx, 5), "chain_ms": round(t_chain, 5),

@@ -175,8 +175,11 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
 // loads after draining its stores (s_waitcnt vmcnt(0) and a barrier: one CU, one L1, one L2),
 // so no data crosses workgroups and no flag, fence or cache maintenance is needed. The
 // workgroup that stores the call's last TX tile writes the RX history after it.
+// 3 waves per SIMD (<= 168 VGPRs): at 4 the TX tile with its tail sub-tiles and the RX tile
+// in one loop spilled to scratch; 3 workgroups per CU cost the RX and TX kernels little alone
+// (round 1: RX 35.1 vs 35.0 us at 3 vs 4 per CU, TX 28.4 vs 28.1 at 3 vs 5).
 template <int SPS, int NKS_T, int NKS_R, typename T, int EM, int LAG>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<SPS, NKS_R, T, MIX_COMPLEX, T, 4>::WPE)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 void chain_flow(const TxParams tp, const th8* __restrict__ bfrag, const RxParams rp,
                 const _Float16* __restrict__ tables, const ChainGeo g) {
     using TK = TxMfma<SPS, NKS_T, OUT_IQ_MIXED, T, 4>;
@@ -184,13 +187,6 @@ void chain_flow(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_f[];
     const int64_t bid = blockIdx.x, nb = gridDim.x;
     if (bid == 0) tx_state_update(tp);
-    const int lane = threadIdx.x & 63;
-    th8 bh[NKS_T], bl[NKS_T];
-#pragma unroll
-    for (int s = 0; s < NKS_T; ++s) {
-        bh[s] = bfrag[(2 * s) * 64 + lane];
-        bl[s] = bfrag[(2 * s + 1) * 64 + lane];
-    }
     _Float16* pl = lds_f;
     _Float16* pl2 = lds_f + TK::PLANES;
     th4* lut_s = reinterpret_cast<th4*>(lds_f + 2 * TK::PLANES);
@@ -200,6 +196,17 @@ void chain_flow(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
     const bool fastb = tp.fast_bits && tp.exact_idx;
     for (int64_t t = bid; t < g.ntx + LAG * nb; t += nb) {
         if (t < g.ntx) {
+            // the B fragments are reloaded per TX tile (L2-resident): kept live across the RX
+            // tile they pushed the kernel past 128 VGPRs into scratch; the opaque lane index
+            // stops the compiler from hoisting the loads out of the loop
+            int lane = threadIdx.x & 63;
+            asm volatile("" : "+v"(lane));
+            th8 bh[NKS_T], bl[NKS_T];
+#pragma unroll
+            for (int s = 0; s < NKS_T; ++s) {
+                bh[s] = bfrag[(2 * s) * 64 + lane];
+                bl[s] = bfrag[(2 * s + 1) * 64 + lane];
+            }
             bool done = false;
             if (fastb) {
                 done = true;
