@@ -578,8 +578,6 @@ static int64_t tx_nt_below(int64_t nsamp, uint64_t launch_bytes) {
 static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool flush, void* dout,
                     int64_t nsym, int ncarry_new, size_t nsamp, mk::TxParams& p) {
     p.bits = dbits;
-    static const int bal = [] { const char* e = std::getenv("MODEM_TX_BAL"); return e ? std::atoi(e) : 0; }();
-    p.bal = bal;
     p.carry = h->d_carry[h->ccur];
     p.carry_new = h->d_carry[h->ccur ^ 1];
     p.hist = h->d_hist[h->hcur];

@@ -61,7 +61,6 @@ struct TxParams {
     float ph_shift;
     int32_t ph_map;
     float ph_max;
-    int32_t bal;             // tx_mfma: uneven rounds (MODEM_TX_BAL, experiment)
 };
 
 // One RX launch: input samples [0, N) (stream indices n_start ..), outputs k_first ..

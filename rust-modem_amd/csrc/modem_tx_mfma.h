@@ -525,30 +525,17 @@ __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __res
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
     // tiles bid, bid + nb, ...: concurrently running workgroups work on neighbouring tiles
     // (measured 1 % faster on C3 than contiguous ranges per workgroup)
-    const int64_t t0 = bid, ts = nb;
-    int64_t t1 = ntiles, tx = -1;
-    // Uneven rounds (p.bal, experiment; as rx_mfma_body): the last quarter of the grid hands its
-    // last-round tile to the first quarter, which runs it after its own (same XCD slot).
-    const int64_t R = (ntiles + nb - 1) / nb;
-    if (p.bal && nb % 32 == 0 && ntiles == R * nb && R >= 2) {
-        const int64_t qn = nb / 4;
-        if (bid >= nb - qn) t1 = (R - 1) * nb;
-        else if (bid < qn) tx = (R - 1) * nb + (nb - qn) + bid;
-    }
+    const int64_t t0 = bid, t1 = ntiles, ts = nb;
     if (t0 >= t1) return;
-    auto go = [&](int64_t a, int64_t b, int64_t st) {
-        if (p.fast_bits && p.exact_idx) {          // one uniform switch: the tile loop is specialised
-            switch (p.bps) {
-            case 1: K::template run<1>(p, pl, lut_s, bh, bl, a, b, st); return;
-            case 2: K::template run<2>(p, pl, lut_s, bh, bl, a, b, st); return;
-            case 4: K::template run<4>(p, pl, lut_s, bh, bl, a, b, st); return;
-            case 8: K::template run<8>(p, pl, lut_s, bh, bl, a, b, st); return;
-            }
+    if (p.fast_bits && p.exact_idx) {              // one uniform switch: the tile loop is specialised
+        switch (p.bps) {
+        case 1: K::template run<1>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 2: K::template run<2>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 4: K::template run<4>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 8: K::template run<8>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
         }
-        K::template run<0>(p, pl, lut_s, bh, bl, a, b, st);
-    };
-    go(t0, t1, ts);
-    if (tx >= 0) go(tx, tx + 1, 1);
+    }
+    K::template run<0>(p, pl, lut_s, bh, bl, t0, t1, ts);
 }
 
 // Tile size by the work: 4 sub-tiles per wave when the call has at least four such tiles
