@@ -938,8 +938,6 @@ static void rx_fill(const modem_rx* h, const void* din, size_t n, void* diq, uin
     p.exact_idx = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL) <= (1ull << 53) ? 1 : 0;
     p.idx46 = (h->c0 + (uint64_t)h->consumed + n + (uint64_t)h->HL + 65536) < (1ull << 46) ? 1 : 0;
     p.ka_in = h->d_ka + h->hcur;
-    static const int bal = [] { const char* e = std::getenv("MODEM_RX_BAL"); return e ? std::atoi(e) : 0; }();
-    p.bal = bal;
     p.ka_out = h->d_ka + (h->hcur ^ 1);
     p.slicer_kind = h->slicer.kind;
     p.bps = (int)h->slicer.bits_per_symbol;

@@ -95,7 +95,6 @@ struct RxParams {
     int32_t idx46;           // every carrier index of this call is < 2^46 (rx_mfma's f32 index split)
     const int* ka_in;        // rx_mfma: staging exponent the previous call ended with (INT_MIN: none)
     int* ka_out;             // rx_mfma: the one this call ends with (written with its last tile)
-    int32_t bal;             // rx_mfma: uneven rounds (MODEM_RX_BAL, experiment)
 };
 
 struct FirParams {

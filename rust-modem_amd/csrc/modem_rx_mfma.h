@@ -258,9 +258,7 @@ __device__ __forceinline__ int f32_exp(float m) { return (int)((__float_as_uint(
 
 // The tiles one workgroup runs, in order: first, first + step, ... (count of them), of the
 // call's ntiles.
-// `extra` >= 0: one more tile, run before `first` (the uneven rounds of rx_mfma_body; it lies
-// above every tile of the progression, so the walk stays top-down).
-struct TileSeq { int64_t first, step, count, ntiles, extra = -1; };
+struct TileSeq { int64_t first, step, count, ntiles; };
 
 // The fused small call's hand-off (RxMfma::run<EM, true>): the LDS copy of the samples the
 // workgroup's TX emitted, call samples [base, base + n), and the value of *ka_in.
@@ -734,29 +732,20 @@ struct RxMfma {
     // tiles with q >= 0 and t * TS >= lead come first).
     struct Walk {
         int64_t t, q, step, dq, last;          // tile, q_lo_of(t), steps per tile, the call's last tile
-        int64_t jt, jq;                        // after an extra first tile: the progression's first
         int32_t i, count, nfull;               // position, tiles in the walk, leading full tiles
-        __device__ void next() {
-            ++i;
-            if (jt >= 0) { t = jt; q = jq; jt = -1; }
-            else { t += step; q += dq; }
-        }
+        __device__ void next() { ++i; t += step; q += dq; }
         __device__ bool full() const { return i < nfull; }
-        __device__ int64_t next_q() const { return jt >= 0 ? jq : q + dq; }
         __device__ bool next_full() const { return i + 1 < nfull && i + 1 < count; }
     };
     __device__ static Walk walk(const RxParams& p, const TileSeq& sq, bool fast) {
         Walk w;
-        const bool ex = sq.extra >= 0;
-        w.t = ex ? sq.extra : sq.first;
+        w.t = sq.first;
         w.step = sq.step;
         w.dq = sq.step * (int64_t)(TS * DEC);
-        w.q = q_lo_of(p, w.t);
-        w.jt = ex ? sq.first : -1;
-        w.jq = ex ? q_lo_of(p, sq.first) : 0;
+        w.q = q_lo_of(p, sq.first);
         w.last = sq.ntiles - 1;
         w.i = 0;
-        w.count = (int32_t)sq.count + (ex ? 1 : 0);
+        w.count = (int32_t)sq.count;
         w.nfull = 0;
         if (fast) {                            // the smallest full tile: q_lo_of(t) >= 0, t * TS >= lead
             const int64_t q0 = q_lo_of(p, 0);
@@ -766,7 +755,6 @@ struct RxMfma {
                 const int64_t n = (sq.first - tmin) / -sq.step + 1;
                 w.nfull = (int32_t)(n < sq.count ? n : sq.count);
             }
-            if (ex && sq.extra >= tmin) w.nfull = sq.first >= tmin ? w.nfull + 1 : 1;
         }
         return w;
     }
@@ -783,7 +771,7 @@ struct RxMfma {
             const int64_t t = w.t;
             const bool fi = w.full();
             const bool pf = w.next_full();
-            const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? w.next_q() : 0, pf);
+            const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? w.q + w.dq : 0, pf);
             const Idx ix = idx_split(p.c0 + (uint64_t)(w.q + p.n_start));
             // the staging (VALU-bound, the limiting stage) issues ahead of the other
             // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
@@ -926,15 +914,6 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
     const int64_t R = (ntiles + nb - 1) / nb * nb;
     TileSeq sq{R - nb + bid, -nb, R / nb, ntiles};
     if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }
-    // Uneven rounds (p.bal, experiment): issue arbitration on a CU favours the waves dealt
-    // first, so the last quarter of the grid (the last workgroup dealt to each CU) hands its
-    // top tile to the first quarter, which runs it before its own; the tile stays on its XCD
-    // slot (nb / 4 is a multiple of 8).
-    if (p.bal && nb % 32 == 0 && ntiles == R && R / nb >= 2) {
-        const int64_t qn = nb / 4;
-        if (bid >= nb - qn) { sq.first -= nb; --sq.count; }
-        else if (bid < qn) sq.extra = R - nb + (nb - qn) + bid;
-    }
     if (sq.count <= 0) return;
     K::template run<EM>(p, pl, tbl, tables, red, sq, bid);
 }
