@@ -169,10 +169,6 @@ __device__ __forceinline__ void shift_in(cf2 (&win)[R], cf2 v) {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// s_waitcnt vmcnt(0) as the compiler's own instruction: its waitcnt pass then knows that every
-// pending vector-memory load has returned (an asm wait would be opaque to it).
-__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
-
 // Keep a loaded value in its register: an opaque asm use stops the compiler from
 // rematerialising the load inside a tile loop (where its vmcnt wait would also drain the
 // next tile's prefetch, since vector-memory counters retire in issue order).

@@ -196,10 +196,6 @@ enum { RXE_GEN = 0, RXE_IQ = 1, RXE_SYM = 2, RXE_IQSYM = 3, RXE_NEAREST = 4 };  
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-
-#ifndef MODEM_X_RXWAIT
-#define MODEM_X_RXWAIT 0
-#endif
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
@@ -789,7 +785,6 @@ struct RxMfma {
             f32x4 dre, dim;
             if (NWF == NW || wave < NWF) {     // uniform
                 fir(pl, tbl, dre, dim);
-                if (MODEM_X_RXWAIT) vm_drain();
                 emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
             }
             __syncthreads();                   // the planes are restaged next
@@ -875,7 +870,6 @@ struct RxMfma {
             kpred = read_ka(reds);
             __syncthreads();
         }
-        if (MODEM_X_RXWAIT) vm_drain();
         while (w.i < w.count) {
             if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
             else loop<true, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
@@ -890,7 +884,6 @@ struct RxMfma {
                 // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
                 // not held across the general path, which has no registers to spare)
                 prefetch(w.q, w.i < w.count && w.full());
-                if (MODEM_X_RXWAIT) vm_drain();
             }
         }
     }

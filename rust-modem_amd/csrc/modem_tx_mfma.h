@@ -85,10 +85,6 @@ __device__ __forceinline__ uint32_t word_index(uint64_t v, int bps) {
 // (lead = symbols before this call, mod SB), so a symbol always meets the same taps at the
 // same k positions and a stream cut into calls gives the same samples as one call.
 // Sample-and-hold (no taps) stays on the exact VALU kernels.
-#ifndef MODEM_X_TXWAIT
-#define MODEM_X_TXWAIT -1
-#endif
-
 template <int SPS, int SUB_> struct TxMfmaCfg {
     static constexpr int SB = 16 / SPS;          // symbols per row-block
     static constexpr int NT = 256;               // 4 waves
@@ -476,7 +472,6 @@ struct TxMfma {
             if (full(t)) {
                 if (!ready) prefetch(t);
                 ready = false;
-                if (MODEM_X_TXWAIT >= 0) vm_drain();
                 for (; t < t1 && full(t); t += ts) {
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
@@ -494,7 +489,6 @@ struct TxMfma {
                         // the epilogue (carrier phase, sin/cos, mix, stores) issues ahead
                         // of the other workgroups' staging and filter: +0.6 % C3 bench in
                         // three interleaved pairs (profiles/r02_store_layout_ab.txt)
-                        if (q == MODEM_X_TXWAIT && t + ts < t1) vm_drain();
                         __builtin_amdgcn_s_setprio(1);
                         emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                         __builtin_amdgcn_s_setprio(0);
