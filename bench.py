@@ -425,11 +425,11 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
     b_moved = b_tx + b_rx - (nsamp_launch * S if fused == 2 else 0)
     if fused == 2:
         dom = ("chain (fused TX+RX launch, samples handed to the RX in LDS: buffer written, not re-read)",
-               t_chain, b_moved)
+               t_chain, b_moved, "chain")
     elif fused:
-        dom = ("chain (fused TX+RX launch, RX re-reads the sample buffer)", t_chain, b_moved)
+        dom = ("chain (fused TX+RX launch, RX re-reads the sample buffer)", t_chain, b_moved, "chain")
     else:
-        dom = ("rx", t_rx, b_rx) if t_rx >= t_tx else ("tx", t_tx, b_tx)
+        dom = ("rx", t_rx, b_rx, "rx") if t_rx >= t_tx else ("tx", t_tx, b_tx, "tx")
     two = None
     if fused and hasattr(r, "two_launch_chain_ms"):
         t_two = r.two_launch_chain_ms()
@@ -440,7 +440,11 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
                        "MODEM_CHAIN_FUSED=0), HIP events, priced at the algorithmic bytes"}
     achieved = dom[2] / (dom[1] * 1e-3) / 1e9
     traffic = pmc_traffic(args.config)
-    dom_traffic = traffic.get(dom[0]) if isinstance(traffic, dict) else None
+    # PMC bytes of the dominant kernel per launch (profiles/pmc_traffic.json; for a fused chain only
+    # when its entry was measured on the same form)
+    dom_traffic = traffic.get(dom[3]) if isinstance(traffic, dict) else None
+    if dom[3] == "chain" and isinstance(traffic, dict) and traffic.get("chain_form") != fused:
+        dom_traffic = None
     chain_gbs = b_moved / (t_chain * 1e-3) / 1e9
     out = {
         "metric": METRIC,
