@@ -217,18 +217,6 @@ __device__ __forceinline__ cf2 cmix(cf2 x, cf2 cssn) {
     return __builtin_elementwise_fma(x.yx, (cf2){cssn.y, -cssn.y}, t);
 }
 
-#ifndef MODEM_RX_STAGE_G
-#define MODEM_RX_STAGE_G 1
-#endif
-// f(integral_constant<I>) for I in [B, E), unrolled at compile time.
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (B < E) {
-        f(std::integral_constant<int, B>());
-        static_for<B + 1, E>(f);
-    }
-}
-
 // Four consecutive input samples (one lane's staging quad).
 template <typename InT> struct Quad;
 template <> struct Quad<float> {
@@ -530,64 +518,40 @@ struct RxMfma {
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const float roff = p.phase_offset * kRcp2Pi;          // rx_sincos: carrier + PLL offset, in turns
         float mx = 0.f;
-        // G slots at a time, their steps side by side (independent dependency chains for the
-        // scheduler to interleave), then their reloads
-        auto group = [&](auto uc, auto gc) {
-            constexpr int U0 = decltype(uc)::value, G = decltype(gc)::value;
-            float2 x[G][4];
-            cf4 nf[G], rv[G];
-            float sn[G][4], cs[G][4], zr[G][4], zi[G][4];
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                Q::split(pre[U0 + g], x[g]);
-                const float bu = bl + (float)(4 * NT * (U0 + g));
-                nf[g] = (bu + (cf4){0.f, 1.f, 2.f, 3.f}) + ix.a;    // exact, then one rounding
+        for (int u = 0; u < U; ++u) {
+            if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) {   // partial last slot: not this wave's
+                pre[u] = load_slot(nxt, voff, u);
+                continue;
             }
+            float2 x[4];
+            Q::split(pre[u], x);
+            const int e0 = 4 * (tid + NT * u);
+            const float bu = bl + (float)(4 * NT * u);
+            const cf4 nf = (bu + (cf4){0.f, 1.f, 2.f, 3.f}) + ix.a;   // exact, then one rounding
+            const cf4 rv = __builtin_elementwise_fma(phase_from_f4(p.w, nf), (cf4){kRcp2Pi, kRcp2Pi, kRcp2Pi, kRcp2Pi},
+                                                     (cf4){roff, roff, roff, roff});
+            const float sn[4] = {__builtin_amdgcn_sinf(rv.x), __builtin_amdgcn_sinf(rv.y),
+                                 __builtin_amdgcn_sinf(rv.z), __builtin_amdgcn_sinf(rv.w)};
+            const float cs[4] = {__builtin_amdgcn_cosf(rv.x), __builtin_amdgcn_cosf(rv.y),
+                                 __builtin_amdgcn_cosf(rv.z), __builtin_amdgcn_cosf(rv.w)};
+            float zr[4], zi[4];
 #pragma unroll
-            for (int g = 0; g < G; ++g)
-                rv[g] = __builtin_elementwise_fma(phase_from_f4(p.w, nf[g]), (cf4){kRcp2Pi, kRcp2Pi, kRcp2Pi, kRcp2Pi},
-                                                  (cf4){roff, roff, roff, roff});
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                sn[g][0] = __builtin_amdgcn_sinf(rv[g].x); sn[g][1] = __builtin_amdgcn_sinf(rv[g].y);
-                sn[g][2] = __builtin_amdgcn_sinf(rv[g].z); sn[g][3] = __builtin_amdgcn_sinf(rv[g].w);
-                cs[g][0] = __builtin_amdgcn_cosf(rv[g].x); cs[g][1] = __builtin_amdgcn_cosf(rv[g].y);
-                cs[g][2] = __builtin_amdgcn_cosf(rv[g].z); cs[g][3] = __builtin_amdgcn_cosf(rv[g].w);
+            for (int j = 0; j < 4; ++j) {
+                cf2 z = MIX == MIX_REFERENCE_REAL ? (cf2){x[j].x * cs[j], x[j].x * -sn[j]}
+                                                  : cmix((cf2){x[j].x, x[j].y}, (cf2){cs[j], sn[j]});
+                if (SC) z = z * sc;
+                zr[j] = z.x;
+                zi[j] = z.y;
+                // only the last slot can reach past the tile: its extra samples are not counted
+                if ((u + 1) * 4 * NT <= NS || e0 + j < NS)
+                    asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[j]), "v"(zi[j]));
             }
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const int u = U0 + g;
-                const int e0 = 4 * (tid + NT * u);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    cf2 z = MIX == MIX_REFERENCE_REAL ? (cf2){x[g][j].x * cs[g][j], x[g][j].x * -sn[g][j]}
-                                                      : cmix((cf2){x[g][j].x, x[g][j].y}, (cf2){cs[g][j], sn[g][j]});
-                    if (SC) z = z * sc;
-                    zr[g][j] = z.x;
-                    zi[g][j] = z.y;
-                    // only the last slot can reach past the tile: its extra samples are not counted
-                    if ((u + 1) * 4 * NT <= NS || e0 + j < NS)
-                        asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(zr[g][j]), "v"(zi[g][j]));
-                }
-                if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, pos0 + u * SLOT_POS, zr[g], zi[g]);
-            }
-            // (not hoisted above the mix: the slots' registers would be copied out first)
+            if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, pos0 + u * SLOT_POS, zr, zi);
+            // (not hoisted above the mix: the slot's registers would be copied out first)
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int g = 0; g < G; ++g) pre[U0 + g] = load_slot(nxt, voff, U0 + g);   // the next tile's slots
-            __builtin_amdgcn_sched_barrier(0);                 // one group's temporaries at a time
-        };
-        // the slots every wave stages in full, G = MODEM_RX_STAGE_G at a time, then the partial last
-        // slot (staged only by the waves whose quads it holds)
-        constexpr int UF = NQ / NT;                            // full slots
-        constexpr int GS = MODEM_RX_STAGE_G;
-        static_for<0, UF / GS>([&](auto k) { group(std::integral_constant<int, decltype(k)::value * GS>(),
-                                                   std::integral_constant<int, GS>()); });
-        static_for<0, UF % GS>([&](auto k) { group(std::integral_constant<int, UF / GS * GS + decltype(k)::value>(),
-                                                   std::integral_constant<int, 1>()); });
-        if constexpr (UF < U) {
-            if (64 * wave + NT * UF >= NQ) pre[UF] = load_slot(nxt, voff, UF);   // not this wave's
-            else group(std::integral_constant<int, UF>(), std::integral_constant<int, 1>());
+            pre[u] = load_slot(nxt, voff, u);                  // the next tile's slot u, same registers
+            __builtin_amdgcn_sched_barrier(0);                 // one quad's temporaries at a time
         }
         // three votes per wave instead of a max reduction
         const bool blo = __ballot(mx >= win.x) != 0, bhi = __ballot(mx >= win.y) != 0,
