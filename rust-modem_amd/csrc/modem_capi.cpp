@@ -571,7 +571,9 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
 static int64_t tx_nt_below(int64_t nsamp, uint64_t launch_bytes) {
     static const int mode = [] { const char* e = std::getenv("MODEM_TX_NT"); return e ? std::atoi(e) : 1; }();
     constexpr uint64_t kMin = 192ull << 20;
-    return mode != 0 && launch_bytes > kMin && nsamp > 0 ? nsamp : 0;
+    if (mode == 0 || launch_bytes <= kMin || nsamp <= 0) return 0;
+    // MODEM_TX_NT=k > 1 (experiment): only the first (k-1)/k of the samples non-temporally
+    return mode > 1 ? nsamp / mode * (mode - 1) : nsamp;
 }
 
 // Kernel parameters of one TX call on device buffers (dbits, dout); see tx_run.
