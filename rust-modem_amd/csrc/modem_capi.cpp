@@ -565,15 +565,19 @@ modem_status modem_tx_create(const modem_tx_desc* d, int device, modem_tx** out)
 // (profiles/r03_tx_nt.txt, bench legs): C5 chain 280.9 -> 268.5 us, TX alone 135 -> 109 us,
 // the RX in the chain 145.5 -> 159.5 us (it now reads everything from HBM); C4 chain 121 ->
 // 116.6 us. (The earlier compile-time all-NT build measured C5 chain 273.4 -> 257.9 us on
-// another box; keeping the last 128 MiB cacheable, 261.4.) Smaller launches (C3: 128 MiB, whose RX
-// re-reads it from the cache) keep the default policy. MODEM_TX_NT=0 turns it off (A/B).
+// another box; keeping the last 128 MiB cacheable, 261.4.) A single-channel launch of at most
+// the Infinity Cache's size (C5 f16: 256 MiB) stores only its first half non-temporally: the
+// RX, walking its tiles top-down, then finds the second half in the cache (chain 182.6 ->
+// 178.3-179.2 us, profiles/r04_tx_nt.txt; the same split for C5 f32 and for C4's 8-channel
+// batch was slower: 265 vs 261 us, 125.8 vs 120 us). Smaller launches (C3: 128 MiB, whose RX
+// re-reads it from the cache) keep the default policy. MODEM_TX_NT=0 turns it off (A/B),
+// MODEM_TX_NT=1 stores every large launch's samples non-temporally.
 // `launch_bytes`: the whole launch's output (every channel of a batch); returns nt_below.
-static int64_t tx_nt_below(int64_t nsamp, uint64_t launch_bytes) {
-    static const int mode = [] { const char* e = std::getenv("MODEM_TX_NT"); return e ? std::atoi(e) : 1; }();
-    constexpr uint64_t kMin = 192ull << 20;
+static int64_t tx_nt_below(int64_t nsamp, uint64_t launch_bytes, bool single) {
+    static const int mode = [] { const char* e = std::getenv("MODEM_TX_NT"); return e ? std::atoi(e) : 2; }();
+    constexpr uint64_t kMin = 192ull << 20, kCache = 256ull << 20;
     if (mode == 0 || launch_bytes <= kMin || nsamp <= 0) return 0;
-    // MODEM_TX_NT=k > 1 (experiment): only the first (k-1)/k of the samples non-temporally
-    return mode > 1 ? nsamp / mode * (mode - 1) : nsamp;
+    return mode == 2 && single && launch_bytes <= kCache ? nsamp / 2 : nsamp;
 }
 
 // Kernel parameters of one TX call on device buffers (dbits, dout); see tx_run.
@@ -588,7 +592,7 @@ static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool 
     p.taps = h->d_taps;
     p.taps_q = h->d_taps_q;
     p.out = dout;
-    p.nt_below = tx_nt_below((int64_t)nsamp, (uint64_t)nsamp * tx_sample_bytes(h));
+    p.nt_below = tx_nt_below((int64_t)nsamp, (uint64_t)nsamp * tx_sample_bytes(h), true);
     p.s0 = h->sample;
     p.nsym = nsym;
     p.nsym_valid = flush ? 0 : nsym;
@@ -753,7 +757,7 @@ modem_status modem_tx_process_batch(modem_tx* const* hs, size_t nch, const uint8
         for (int i = 0; i < b.nch; ++i)
             launch_bytes += (uint64_t)nsym[c0 + i] * hs[c0 + i]->sps * tx_sample_bytes(hs[c0 + i]);
         for (int i = 0; i < b.nch; ++i)
-            b.p[i].nt_below = tx_nt_below(nsym[c0 + i] * (int64_t)hs[c0 + i]->sps, launch_bytes);
+            b.p[i].nt_below = tx_nt_below(nsym[c0 + i] * (int64_t)hs[c0 + i]->sps, launch_bytes, false);
         HIP_TRY(mk::launch_tx_mfma_batch(b, (int)hs[0]->sps, hs[0]->mfma_ksteps, hs[0]->d_bfrag, hs[0]->dtype, s));
         for (int i = 0; i < b.nch; ++i) {
             const size_t c = c0 + (size_t)i;

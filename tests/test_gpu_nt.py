@@ -1,6 +1,7 @@
 """Non-temporal TX stores (rust-modem_amd/csrc/modem_capi.cpp tx_nt_below): a TX launch whose
-output exceeds 192 MiB (past the 256 MiB Infinity Cache) stores its samples non-temporally.
-The store policy must not change a single sample:
+output exceeds 192 MiB stores its samples non-temporally (a single-channel launch of at most
+256 MiB, as here, its first half: both store paths in one call). The store policy must not
+change a single sample:
 
   * C5's filter (256-QAM, 513 taps, sps 8) over 256 MiB of I/Q (2^25 f32 or 2^26 f16 samples:
     the non-temporal form) equals, bit for bit, the same stream produced by two calls of half
