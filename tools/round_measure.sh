@@ -9,11 +9,13 @@ root=${GRAFT_REPO_ROOT:-$(pwd)}
 out="$root/gpurun_out/$tag"
 mkdir -p "$out"
 cd "$root"
-echo "[1/5] gpu tests"
-timeout -k 10 420 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > "$out/gpu_tests.log" 2>&1 || { tail -30 "$out/gpu_tests.log"; exit 1; }
+echo "[1/5] gpu tests, smoke"
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > "$out/gpu_tests.log" 2>&1 || { tail -30 "$out/gpu_tests.log"; exit 1; }
 tail -1 "$out/gpu_tests.log"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || { tail -20 "$out/smoke.log"; exit 1; }
+tail -2 "$out/smoke.log"
 echo "[2/5] bench, driver style (20 + 5 steps) x2, then defaults"
-for k in 1 2; do
+for k in 1 2 3; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$out/bench_drv$k.json" 2> "$out/bench_drv$k.err" || { tail -20 "$out/bench_drv$k.err"; exit 2; }
   python3 -c "import json;d=json.load(open('$out/bench_drv$k.json'));r=d['roofline'];c=d['chain_roofline'];print('drv$k',d['value'],d['ms_per_step'],r['kernel'],r['frac'],c['tx_ms'],c['rx_ms'],c['chain_ms'],c['frac'],d['decisions_match_sent'])"
 done
