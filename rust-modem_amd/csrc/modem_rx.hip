@@ -172,21 +172,21 @@ __global__ __launch_bounds__(256) void rx_fast(const RxParams p) {
     }
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NWF>::WPE)))
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM, int KS>
+__global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NWF, KS>::WPE)))
 void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM>(p, tables, blockIdx.x, gridDim.x);
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>(p, tables, blockIdx.x, gridDim.x);
 }
 
 // A batch of independent channels of one configuration (modem_rx_process_batch): workgroup
 // b serves channel b / g as its workgroup b % g of g.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NWF>::WPE)))
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM, int KS>
+__global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NWF, KS>::WPE)))
 void rx_mfma_batch(const RxBatch b, const _Float16* __restrict__ tables) {
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
     const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
     const RxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM>(p, tables, bid, b.g);
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>(p, tables, bid, b.g);
 }
 
 // Any decimation: thread per kept instant, mixed samples staged in natural order.
@@ -303,32 +303,39 @@ static hipError_t rx_mixsel(const RxParams& p, int decim, int mix, hipStream_t s
 }
 
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM, int KS>
 static hipError_t rxm_go_em(const RxParams& p, const void* tables, hipStream_t s) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF, KS>;
     const int64_t ntiles = (p.nout + (p.k_first & 15) + K::TS - 1) / K::TS;
-    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM>);
-    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM>), dim3(persistent_grid(k, K::NT, K::LDS_BYTES, ntiles)),
+    const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>);
+    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>), dim3(persistent_grid(k, K::NT, K::LDS_BYTES, ntiles)),
                        dim3(K::NT), K::LDS_BYTES, s, p, static_cast<const _Float16*>(tables));
     return hipGetLastError();
 }
 
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM, int KS>
 static hipError_t rxm_go_batch_em(RxBatch b, const void* tables, hipStream_t s) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF, KS>;
     int64_t ntiles = 0;
     for (int c = 0; c < b.nch; ++c) {
         const int64_t t = (b.p[c].nout + (b.p[c].k_first & 15) + K::TS - 1) / K::TS;
         ntiles = t > ntiles ? t : ntiles;
     }
-    const void* k = reinterpret_cast<const void*>(&rx_mfma_batch<DEC, NKS, InT, MIX, OutT, NWF, EM>);
+    const void* k = reinterpret_cast<const void*>(&rx_mfma_batch<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>);
     const int64_t cap = persistent_grid(k, K::NT, K::LDS_BYTES, INT64_MAX);
     int64_t g = cap / b.nch;
     g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
     b.g = (int32_t)g;
-    hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX, OutT, NWF, EM>), dim3((unsigned)(g * b.nch)),
+    hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>), dim3((unsigned)(g * b.nch)),
                        dim3(K::NT), K::LDS_BYTES, s, b, static_cast<const _Float16*>(tables));
     return hipGetLastError();
+}
+
+// The K-split launch (RxMfma KS = 2) for the 1024-instant tiles of the configurations that
+// have one; MODEM_RX_KSPLIT=0 runs them with KS = 1 (the same results: RxMfma::KSO).
+static bool rx_ksplit() {
+    static const bool on = [] { const char* e = std::getenv("MODEM_RX_KSPLIT"); return !e || std::atoi(e) != 0; }();
+    return on;
 }
 
 // Dispatch on the epilogue (the specialised ones exist only where rx_mfma_em can pick them)
@@ -337,14 +344,18 @@ template <int DEC, int NKS, typename InT, int MIX, typename OutT, bool BATCH, ty
 static hipError_t rxm_em(const Arg& a, int em, bool small, const void* tables, hipStream_t s) {
     constexpr bool loop = std::is_same<InT, OutT>::value && MIX == MIX_COMPLEX;
     constexpr bool f32 = std::is_same<InT, float>::value;
+    constexpr int KS = RxMfma<DEC, NKS, InT, MIX, OutT, 4>::KSO ? 2 : 1;
     auto go = [&](auto emc) {
         constexpr int E = decltype(emc)::value;
+        const bool ks = KS > 1 && rx_ksplit();
         if constexpr (BATCH)
-            return small ? rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, 1, E>(a, tables, s)
-                         : rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, 4, E>(a, tables, s);
+            return small ? rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, 1, E, 1>(a, tables, s)
+                 : ks    ? rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, 4, E, KS>(a, tables, s)
+                         : rxm_go_batch_em<DEC, NKS, InT, MIX, OutT, 4, E, 1>(a, tables, s);
         else
-            return small ? rxm_go_em<DEC, NKS, InT, MIX, OutT, 1, E>(a, tables, s)
-                         : rxm_go_em<DEC, NKS, InT, MIX, OutT, 4, E>(a, tables, s);
+            return small ? rxm_go_em<DEC, NKS, InT, MIX, OutT, 1, E, 1>(a, tables, s)
+                 : ks    ? rxm_go_em<DEC, NKS, InT, MIX, OutT, 4, E, KS>(a, tables, s)
+                         : rxm_go_em<DEC, NKS, InT, MIX, OutT, 4, E, 1>(a, tables, s);
     };
     switch (em) {
     case RXE_IQSYM: return go(std::integral_constant<int, loop ? RXE_IQSYM : RXE_GEN>());

@@ -311,13 +311,17 @@ __device__ __forceinline__ uint8_t rx_slice_qam2(const RxParams& p, float re, fl
 // wave votes with three ballots whether the tile's max lies in that exponent's window. A tile
 // outside it, and the call's first tile (its window reads the history), take the general
 // path: per-sample loads, two passes, the same tile_ka -> identical results either way.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF_ = 4>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF_ = 4, int KS_ = 1>
 struct RxMfma {
     using Q = Quad<InT>;
     using QT = typename Q::T;
-    static constexpr int NT = 256;                              // 4 waves stage every tile
+    // K-split (KS = 2): two waves per 16-row block, each summing half of its k-steps, the upper
+    // wave's sums handed over in LDS; 8 waves stage and filter a tile, so a tile whose planes
+    // leave room for only 2 workgroups per CU (C5 f32: 73 KB) still runs 4 waves per SIMD.
+    static constexpr int KS = KS_;
+    static constexpr int NT = 256 * KS;                         // 4 (KS = 2: 8) waves stage every tile
     static constexpr int NW = NT / 64;
-    static constexpr int NWF = NWF_;                            // of which NWF filter it: 4, or 1 (small calls)
+    static constexpr int NWF = NWF_;                            // 16-row blocks per tile: 4, or 1 (small calls)
     static constexpr int TS = NWF * 256;                        // kept instants per tile
     static constexpr int RW = 16 * DEC;                         // samples per A row
     static constexpr int W = 32 * NKS;
@@ -328,7 +332,7 @@ struct RxMfma {
     // 8 (decim 4) or 16 (decim 8) chunks by the row bits — conflict-free A reads and staging
     // writes (tests/test_lds_banks.py) and no pad halves, which lets 4 workgroups share a CU
     // (decim 4; decim 8 with two planes). Otherwise rxh_pos.
-    static constexpr bool SWZ = (DEC == 4 || DEC == 8) && NT == 256;
+    static constexpr bool SWZ = (DEC == 4 || DEC == 8) && (4 * NT) % 1024 == 0;
     __host__ __device__ static constexpr int ppos(int e) {
         return !SWZ ? rxh_pos(e, RW)
              : DEC == 4 ? ((((e >> 3) ^ (((e >> 7) & 3) << 1)) << 3) | (e & 7))
@@ -343,18 +347,27 @@ struct RxMfma {
     // (re_hi, re_lo, im_hi, im_lo).
     static constexpr bool HI = std::is_same<InT, __half>::value && std::is_same<OutT, __half>::value;
     static constexpr int NPL = HI ? 2 : 4;
+    // The matched filter's summation order: for the configurations a K-split launch may run
+    // (decim 8, >= 16 k-steps, four planes: C5 f32) every launch sums the first and the second
+    // half of the k-steps separately and adds the two, whatever its KS, tile size or kernel
+    // (single-side, chain), so that results still never depend on how a stream is cut into calls.
+    static constexpr bool KSO = DEC == 8 && NKS >= 16 && NKS % 2 == 0 && !HI;
+    static_assert(KS == 1 || (KS == 2 && KSO && NWF == 4), "K-split: C5-shaped f32 tiles only");
     static constexpr int NC = rx_mfma_table_copies(DEC);
     static constexpr int TB = rx_mfma_table_len(DEC, NKS);      // halves per table (hi or lo)
     // the planes, whose LDS the general path also uses for the raw window (NS float2, or NS
     // half2 for f16 input with HI: within NPL * PL halves either way), the tap tables, votes
     static constexpr int TBL_OFF = NPL * PL;                    // halves
-    static constexpr size_t LDS_BYTES = (size_t)TBL_OFF * 2 + (size_t)NC * 2 * TB * 2 + 8 * 4;   // + votes, maxima
+    // + votes, maxima [NW each], and with KS = 2 the upper waves' partial sums (f32x4 re, im per
+    // lane and block)
+    static constexpr size_t PART_BYTES = KS > 1 ? (size_t)2 * NWF * 64 * 16 : 0;
+    static constexpr size_t LDS_BYTES = (size_t)TBL_OFF * 2 + (size_t)NC * 2 * TB * 2 + 2 * NW * 4 + PART_BYTES;
     static constexpr int K_TAB8 = NC * 2 * TB / 8;              // 16-B chunks of the tap tables
     static constexpr float GAIN = MIX == MIX_REFERENCE_REAL ? 2.0f : 1.0f;
     // Waves per SIMD the registers are held to: 4 where the LDS lets 4 workgroups share a CU
     // (the matched filter then single-buffers its operands to fit 128 VGPRs), else the
     // compiler's choice.
-    static constexpr int WPE = SWZ && LDS_BYTES <= 40960 ? 4 : 1;
+    static constexpr int WPE = SWZ && (LDS_BYTES <= 40960 || KS == 2) ? 4 : 1;
     static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
     // plane offset between staging slots (the swizzle repeats every 1024 samples)
     static constexpr int SLOT_POS = SWZ ? 4 * NT : 4 * NT + 16 * (4 * NT / RW);
@@ -441,14 +454,16 @@ struct RxMfma {
     // B[32s + 8g + j][c = i] = T[32s + 8g + j + (15 - c)*DEC] from the table copy that makes
     // the read aligned. WPE 4: one k-step's operands at a time (fewer registers; the other
     // waves hide the LDS latency); otherwise the next k-step's load during this one's MFMAs.
-    __device__ static void fir(const _Float16* pl, const _Float16* tbl, f32x4& dre, f32x4& dim) {
+    // fir_part: k-steps [s0, s0 + NS_) of 16-row block blk, summed from zero.
+    template <int NS_>
+    __device__ static void fir_part(const _Float16* pl, const _Float16* tbl, int blk, int s0, f32x4& dre, f32x4& dim) {
         constexpr bool DB = WPE < 4;
-        const int lane = tid_() & 63, wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        const int lane = tid_() & 63;
         const int i = lane & 15, g = lane >> 4;
-        const int ae = (16 * wave + i) * RW + 8 * g;
+        const int ae = (16 * blk + i) * RW + 8 * g + 32 * s0;
         const int xb = 8 * g + (15 - i) * DEC;
         const int q = xb & 7;
-        const _Float16* brow = tbl + (q / (8 / NC)) * 2 * TB + (xb - q);
+        const _Float16* brow = tbl + (q / (8 / NC)) * 2 * TB + (xb - q) + 32 * s0;
         f32x4 r0 = {0.f, 0.f, 0.f, 0.f}, m0 = r0;
         h8 a[2][4], b[2][2];
         auto load = [&](int s, int c) {
@@ -466,10 +481,10 @@ struct RxMfma {
         };
         if (DB) load(0, 0);
 #pragma unroll
-        for (int s = 0; s < NKS; ++s) {
+        for (int s = 0; s < NS_; ++s) {
             const int c = DB ? s & 1 : 0;
             if (!DB) load(s, 0);
-            else if (s + 1 < NKS) load(s + 1, c ^ 1);
+            else if (s + 1 < NS_) load(s + 1, c ^ 1);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][0], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
@@ -482,6 +497,49 @@ struct RxMfma {
         }
         dre = r0;
         dim = m0;
+    }
+    // The wave's whole block (KS = 1): KSO configurations as the two halves' sums added.
+    __device__ static void fir(const _Float16* pl, const _Float16* tbl, f32x4& dre, f32x4& dim) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        if constexpr (KSO) {
+            f32x4 r1, m1;
+            fir_part<NKS / 2>(pl, tbl, wave, 0, dre, dim);
+            fir_part<NKS / 2>(pl, tbl, wave, NKS / 2, r1, m1);
+            dre += r1;
+            dim += m1;
+        } else {
+            fir_part<NKS>(pl, tbl, wave, 0, dre, dim);
+        }
+    }
+
+    // The tile's matched filter and outputs (instants ot0 + 256 blk ..). KS = 1: waves < NWF
+    // filter their block and store. KS = 2: waves blk and blk + NWF each sum half of block blk's
+    // k-steps (the same two halves fir adds); the upper wave hands its sums over in LDS before a
+    // barrier, after which the planes may be restaged, and the lower wave adds them and stores.
+    template <int EM>
+    __device__ __forceinline__ static void filter_emit(const RxParams& p, const _Float16* pl, const _Float16* tbl,
+                                                       f32x4* part, int64_t ot0, int kab) {
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+        f32x4 dre, dim;
+        if constexpr (KS == 1) {
+            if (NWF == NW || wave < NWF) {     // uniform
+                fir(pl, tbl, dre, dim);
+                emit<EM>(p, ot0 + wave * 256, dre, dim, kab);
+            }
+        } else {
+            const int blk = wave % NWF, kh = wave / NWF;
+            fir_part<NKS / 2>(pl, tbl, blk, kh * (NKS / 2), dre, dim);
+            const int lane = tid_() & 63;
+            f32x4* pr = part + 64 * blk + lane;               // [re | im][block][lane]: 16-B lane stride
+            f32x4* pi = pr + 64 * NWF;
+            if (kh == 1) { *pr = dre; *pi = dim; }
+            __syncthreads();
+            if (kh == 0) {
+                dre += *pr;
+                dim += *pi;
+                emit<EM>(p, ot0 + blk * 256, dre, dim, kab);
+            }
+        }
     }
 
     // Split z (4 samples) and write it at plane offset o (HI: the f16 roundings only).
@@ -607,8 +665,8 @@ struct RxMfma {
     // General path for tile t (all waves): two passes over its samples (max, then tile_ka
     // scale + split), the matched filter, the outputs in range. Returns its tile_ka.
     template <int EM>
-    __device__ __forceinline__ static int slow_tile(const RxParams& p, _Float16* pl, const _Float16* tbl, float* reds, int64_t t,
-                                    int kb, int ld) {
+    __device__ __forceinline__ static int slow_tile(const RxParams& p, _Float16* pl, const _Float16* tbl, float* reds, f32x4* part,
+                                    int64_t t, int kb, int ld) {
         // lane values recomputed here, not hoisted to the kernel entry (where, live across
         // the tile loop, they would spill)
         const int tid = tid_();
@@ -705,11 +763,7 @@ struct RxMfma {
             put4(pl, ppos(e0), a, b);
         }
         __syncthreads();
-        f32x4 dre, dim;
-        if (wave < NWF) {                      // uniform
-            fir(pl, tbl, dre, dim);
-            emit<EM>(p, t * TS + wave * 256 - ld, dre, dim, ka + kb);
-        }
+        filter_emit<EM>(p, pl, tbl, part, t * TS - ld, ka + kb);
         __syncthreads();                       // the planes are restaged next
         return ka;
     }
@@ -762,9 +816,8 @@ struct RxMfma {
     // Tiles from w.i on while their staging exponent keeps its class (SC: nonzero). Returns
     // at the end of the walk, or after the barrier of a tile the general path must redo.
     template <bool SC, int EM>
-    __device__ __forceinline__ static void loop(const RxParams& p, _Float16* pl, const _Float16* tbl, int* votes, Walk& w,
-                                const Ctx& cx, QT (&pre)[U], int kpred) {
-        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    __device__ __forceinline__ static void loop(const RxParams& p, _Float16* pl, const _Float16* tbl, int* votes, f32x4* part,
+                                Walk& w, const Ctx& cx, QT (&pre)[U], int kpred) {
         const float sc = __builtin_ldexpf(1.0f, kpred);
         const cf2 win = window(kpred);
         while (w.i < w.count) {
@@ -782,12 +835,8 @@ struct RxMfma {
             __syncthreads();
             if (!(fi && fast_ok(votes, kpred))) return;
             if (t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
-            f32x4 dre, dim;
-            if (NWF == NW || wave < NWF) {     // uniform
-                fir(pl, tbl, dre, dim);
-                emit<EM>(p, t * TS + wave * 256 - cx.ld, dre, dim, kpred + cx.kb);
-            }
-            __syncthreads();                   // the planes are restaged next
+            filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb);
+            if (KS == 1) __syncthreads();      // the planes are restaged next (KS = 2: in filter_emit)
             w.next();
         }
     }
@@ -802,8 +851,9 @@ struct RxMfma {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         const Ctx cx{p.idx46 && ((uintptr_t)p.x & 3) == 0, p.tap_scale_exp, lead(p)};
         Walk w = walk(p, sq, cx.fast);
-        int* votes = reinterpret_cast<int*>(red);            // [4]
-        float* reds = red + 4;                               // [4]
+        int* votes = reinterpret_cast<int*>(red);            // [NW]
+        float* reds = red + NW;                              // [NW]
+        f32x4* part = reinterpret_cast<f32x4*>(red + 2 * NW);   // KS = 2: [2][NWF][64]
         QT pre[U];
         auto prefetch = [&](int64_t q, bool live) {
             const __amdgpu_buffer_rsrc_t r = window_rsrc(p, live ? q : 0, live);
@@ -871,14 +921,14 @@ struct RxMfma {
             __syncthreads();
         }
         while (w.i < w.count) {
-            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
-            else loop<true, EM>(p, pl, tbl, votes, w, cx, pre, kpred);
+            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, part, w, cx, pre, kpred);
+            else loop<true, EM>(p, pl, tbl, votes, part, w, cx, pre, kpred);
             if (w.i < w.count) {               // tile w.t on the general path (one place in the code)
                 if constexpr (HO) {            // it reads HBM: this workgroup's sample stores first
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     __syncthreads();
                 }
-                kpred = slow_tile<EM>(p, pl, tbl, reds, w.t, cx.kb, cx.ld);
+                kpred = slow_tile<EM>(p, pl, tbl, reds, part, w.t, cx.kb, cx.ld);
                 if (w.t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
                 w.next();
                 // reload the next tile (what the staging of tile i loaded is dropped: `pre` is
@@ -891,10 +941,10 @@ struct RxMfma {
 
 // One channel's share of a launch: workgroup `bid` of `nb` working on channel p, with the
 // epilogue EM chosen on the host (rx_mfma_em): each kernel keeps only its own stores.
-template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM>
+template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM, int KS = 1>
 __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* __restrict__ tables, int64_t bid,
                                              int64_t nb) {
-    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF>;
+    using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF, KS>;
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_h[];
     _Float16* pl = lds_h;                                   // 4 sample planes
     _Float16* tbl = lds_h + K::TBL_OFF;                     // NC x (hi, lo) tap tables
