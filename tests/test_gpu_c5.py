@@ -77,3 +77,37 @@ def test_c5_f32_single_launch_full_size(m, o, torch_cuda):
         assert np.array_equal(host(osym[K0: K0 + cnt]), rsym[:cnt]), f"RX decisions at {A}"
     print(f"\n[c5] one 2^26-sample period: {k} decisions = symbols sent; TX max|d|/max|y| "
           f"{worst_tx:.3g}, RX I/Q {worst_rx:.3g} (bound {BOUND})")
+
+
+def test_c5_ksplit_equals_small_tile_calls(m, o, torch_cuda):
+    """The K-split RX launch (RxMfma KS = 2: C5 f32's 1024-instant tiles, 8 waves, two per 16-row
+    block over half of the k-steps each) against the same stream cut into calls small enough for
+    the 256-instant tiles (one filter wave, KS = 1): I/Q and decisions bit for bit — every launch
+    of this configuration sums the two halves of the k-steps the same way (RxMfma::KSO), so a
+    result never depends on how a stream is cut into calls (demodulator.rs:44-56, fir.rs:18-34)."""
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS["c5_qam256"]
+    n = 1 << 24                                         # 2^21 instants: the 1024-instant tiles
+    parts = 16                                          # 2^17 instants per call: 256-instant tiles
+    w = o.sample_freq(1, 4)
+    taps = m.rrc_taps(L, sps, 0.35)
+    bits = m.prng_bits(0x5EED0005, (n // sps) * bps)
+    tx = m.DigitalModulator(m.Carrier(w), m.QAM(8, 0.0, 1.0), sps, taps)
+    y = tx.process(bits)
+    torch.cuda.synchronize()
+
+    def rx():
+        return m.DemodulatorRx(m.Carrier(w), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                               slicer=m.QAM(8, 0.0, 1.0).slicer())
+    iq1, sy1 = rx().process(y[:n])
+    r = rx()
+    outs = [r.process(y[i * (n // parts):(i + 1) * (n // parts)]) for i in range(parts)]
+    torch.cuda.synchronize()
+    iq2 = torch.cat([a for a, _ in outs])
+    sy2 = torch.cat([b for _, b in outs])
+    assert iq1.shape == iq2.shape and sy1.shape == sy2.shape
+    assert torch.equal(iq1.view(torch.int32), iq2.view(torch.int32)), "I/Q differ between the launch shapes"
+    assert torch.equal(sy1, sy2)
+    H = (L - 1 + sps - 1) // sps
+    sent = sent_symbols(host(bits), bps)
+    assert np.array_equal(host(sy1), sent[:len(sy1)]) and len(sy1) == n // sps - H
