@@ -465,7 +465,8 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
                    "channel_batch": bool(getattr(r, "batch", False)),
                    "ntaps": L, "sps": sps, "bits_per_symbol": bps, "rrc_beta": 0.35,
                    "carrier": "Freq::new(1, 4) (fs/4)", "parallelism": f"{world} independent channel set(s), "
-                   "one per GPU, no collectives"},
+                   "one per GPU, no collectives" + (f" (timing barrier and max over ranks: "
+                                                    f"{dist.td.get_backend()})" if dist is not None else "")},
         "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": dom_traffic,
                      "algorithmic_bytes_per_launch": dom[2], "mean_launch_ms": round(dom[1], 5)},
@@ -692,7 +693,7 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     device = local
-    if world > 1:
+    if wenv is not None:      # under a launcher (any world size, so one rank exercises RCCL too)
         import torch
         import torch.distributed as td
         ndev = torch.cuda.device_count()

@@ -73,3 +73,23 @@ def test_bench_gpus_flag_two_ranks():
     assert g["bytes_per_gpu"] == 8 * ((1 << 22) // 4 - 16) and g["ms"] > 0
     total = (1 << 22) * 8 * 10 * 2
     assert abs(out["value"] - total / (out["ms_per_step"] * 10 / 1e3) / 1e6) <= 0.02 * out["value"]
+
+
+def test_rccl_branch_under_launcher(tmp_path):
+    """The driver's multi-GPU invocation (python -m torch.distributed.run ... bench.py --gpus N)
+    with one rank on the box's GPU: bench.py takes its RCCL branch (init_process_group("nccl")
+    with the rank's device, the device barrier and the max-over-ranks all_reduce on a GPU
+    tensor), the branch every rank of the driver's 8-GPU scaling run takes."""
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "1", "--config", "c2", "--steps", "20", "--warmup", "3", "--settle-ms", "0",
+           "--no-cpu-baseline", "--no-out-of-cache"]
+    r = subprocess.run(cmd, cwd=str(tmp_path), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 1 and out["decisions_match_sent"] is True
+    assert "max over ranks: nccl" in out["config"]["parallelism"], out["config"]["parallelism"]
