@@ -1093,7 +1093,6 @@ modem_status modem_rx_destroy(modem_rx* h) { delete h; return MODEM_OK; }
 // queries and staging decisions, ~1 us of host time each per call).
 struct modem_chain {
     bool fused = true;
-    int flow = 0;              // MODEM_CHAIN_FLOW=1/2: calls at size as one chain_flow launch (lag 0/1)
     int last = -1;             // how the last run ran (modem_chain_fused)
     bool verbose = false;      // MODEM_CHAIN_VERBOSE=1: why a run took the two launches (stderr)
     modem_tx* tx = nullptr;
@@ -1124,8 +1123,6 @@ modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits,
     c->out_iq = out_iq; c->out_sym = out_sym; c->out_cap = out_cap;
     const char* env = std::getenv("MODEM_CHAIN_FUSED");
     c->fused = !(env && env[0] == '0');
-    const char* fl = std::getenv("MODEM_CHAIN_FLOW");
-    c->flow = fl ? std::atoi(fl) : 0;
     const char* verb = std::getenv("MODEM_CHAIN_VERBOSE");
     c->verbose = verb && verb[0] == '1';
     *out = c;
@@ -1163,17 +1160,8 @@ modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_
         mk::RxParams rp{};
         rx_fill(rx, c->samples, nsamp, c->out_iq, c->out_sym, k_first, nout, rp);
         int form = 1;
-        hipError_t e = hipErrorNotSupported;
-        if (c->flow > 0) {
-            e = mk::launch_chain_flow(tp, (int)tx->sps, tx->mfma_ksteps, tx->d_bfrag, rp, rx->mfma_ksteps,
-                                      rx->d_bfrag, tx->dtype, s, c->flow - 1);
-            form = 2 + c->flow;                    // 3: flow, lag 0; 4: flow, lag 1
-        }
-        if (e == hipErrorNotSupported) {
-            form = 1;
-            e = mk::launch_chain_mfma(tp, (int)tx->sps, tx->mfma_ksteps, tx->d_bfrag, rp, rx->mfma_ksteps,
-                                      rx->d_bfrag, tx->dtype, s, &form);
-        }
+        const hipError_t e = mk::launch_chain_mfma(tp, (int)tx->sps, tx->mfma_ksteps, tx->d_bfrag, rp, rx->mfma_ksteps,
+                                                   rx->d_bfrag, tx->dtype, s, &form);
         if (e == hipSuccess) {
             c->last = form;
             tx_advance(tx, false, nsym, ncarry_new, nsamp);

@@ -165,72 +165,6 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
                                RxHandoff{raw, rb, rn, kin});
 }
 
-// The call at size as a flow of tiles (C3: one launch instead of the TX and RX launches).
-// Workgroup b takes TX tiles b, b + G, ... (grid-strided, as tx_mfma) and after TX tile t the
-// RX tile t - LAG*G: LAG 0, the tile it has just written; LAG 1, the one it wrote a round
-// earlier. An RX tile's window reaches H < 256 xs samples back into the previous TX tile, so
-// each TX tile is computed together with the last xs sub-tiles of the tile before it
-// (TxMfma::one_tile: the same values that tile's owner stores there), and every RX window
-// lies in samples the workgroup stored itself; it re-reads them from memory with global
-// loads after draining its stores (s_waitcnt vmcnt(0) and a barrier: one CU, one L1, one L2),
-// so no data crosses workgroups and no flag, fence or cache maintenance is needed. The
-// workgroup that stores the call's last TX tile writes the RX history after it.
-// 3 waves per SIMD (<= 168 VGPRs): at 4 the TX tile with its tail sub-tiles and the RX tile
-// in one loop spilled to scratch; 3 workgroups per CU cost the RX and TX kernels little alone
-// (round 1: RX 35.1 vs 35.0 us at 3 vs 4 per CU, TX 28.4 vs 28.1 at 3 vs 5).
-template <int SPS, int NKS_T, int NKS_R, typename T, int EM, int LAG>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
-void chain_flow(const TxParams tp, const th8* __restrict__ bfrag, const RxParams rp,
-                const _Float16* __restrict__ tables, const ChainGeo g) {
-    using TK = TxMfma<SPS, NKS_T, OUT_IQ_MIXED, T, 4>;
-    using RK = RxMfma<SPS, NKS_R, T, MIX_COMPLEX, T, 4>;
-    extern __shared__ __attribute__((aligned(16))) _Float16 lds_f[];
-    const int64_t bid = blockIdx.x, nb = gridDim.x;
-    if (bid == 0) tx_state_update(tp);
-    _Float16* pl = lds_f;
-    _Float16* pl2 = lds_f + TK::PLANES;
-    th4* lut_s = reinterpret_cast<th4*>(lds_f + 2 * TK::PLANES);
-    _Float16* tbl = lds_f + RK::TBL_OFF;
-    float* red = reinterpret_cast<float*>(tbl + RK::NC * 2 * RK::TB);
-    const RawOut none{nullptr, 0, 0};
-    const bool fastb = tp.fast_bits && tp.exact_idx;
-    for (int64_t t = bid; t < g.ntx + LAG * nb; t += nb) {
-        if (t < g.ntx) {
-            // the B fragments are reloaded per TX tile (L2-resident): kept live across the RX
-            // tile they pushed the kernel past 128 VGPRs into scratch; the opaque lane index
-            // stops the compiler from hoisting the loads out of the loop
-            int lane = threadIdx.x & 63;
-            asm volatile("" : "+v"(lane));
-            th8 bh[NKS_T], bl[NKS_T];
-#pragma unroll
-            for (int s = 0; s < NKS_T; ++s) {
-                bh[s] = bfrag[(2 * s) * 64 + lane];
-                bl[s] = bfrag[(2 * s + 1) * 64 + lane];
-            }
-            bool done = false;
-            if (fastb) {
-                done = true;
-                switch (tp.bps) {
-                case 1: TK::template one_tile<1, false>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, none); break;
-                case 2: TK::template one_tile<2, false>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, none); break;
-                case 4: TK::template one_tile<4, false>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, none); break;
-                case 8: TK::template one_tile<8, false>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, none); break;
-                default: done = false;
-                }
-            }
-            if (!done) TK::template one_tile<0, false>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, none);
-            // every wave's sample stores done before any wave of the workgroup reads them back
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            if (t == g.ntx - 1) rx_state_update<T>(rp);      // the call's last samples: stored above
-        }
-        const int64_t j = t - LAG * nb;
-        if (j >= 0 && j < g.nrx) {
-            const TileSeq sq{j, -1, 1, g.nrx};
-            RK::template run<EM>(rp, lds_f, tbl, tables, red, sq, bid);
-        }
-    }
-}
 
 // Launch geometry, or false when the call does not fit the fused form (the caller then runs
 // the two launches): matching tile sizes (small or not on both sides), RX tiles of m whole
@@ -278,34 +212,6 @@ static hipError_t chain_go_em(const TxParams& tp, const void* bfrag, const RxPar
     return hipGetLastError();
 }
 
-// The flow form's geometry: one TX tile per RX tile (m = 1), every RX window inside its TX
-// tile plus the xs sub-tiles before it, the RX history inside the last TX tile and its tail.
-template <int SPS, int NKS_T, int NKS_R, typename T>
-static bool chain_flow_geo(const TxParams& tp, const RxParams& rp, int64_t grid, ChainGeo& g) {
-    using TK = TxMfma<SPS, NKS_T, OUT_IQ_MIXED, T, 4>;
-    if (!chain_geo<SPS, NKS_T, NKS_R, T, 4>(tp, rp, 1, g) || g.m != 1 || grid < 1) return false;
-    constexpr int64_t TXS = (int64_t)TK::TS * SPS, SUBS = 16 * TK::SB * SPS;
-    const int64_t last = -(int64_t)tp.lead * SPS + (g.ntx - 1) * TXS - (g.ntx > 1 ? g.xs * SUBS : 0);
-    const int64_t first = rp.N - rp.HL > 0 ? rp.N - rp.HL : 0;          // rx_state_update's first read
-    return first >= last;
-}
-
-template <int SPS, int NKS_T, int NKS_R, typename T, int EM, int LAG>
-static hipError_t chain_flow_em(const TxParams& tp, const void* bfrag, const RxParams& rp, const void* tables,
-                                hipStream_t s) {
-    using TK = TxMfma<SPS, NKS_T, OUT_IQ_MIXED, T, 4>;
-    using RK = RxMfma<SPS, NKS_R, T, MIX_COMPLEX, T, 4>;
-    const size_t tx_lds = ((size_t)2 * TK::PLANES + 256 * 4) * 2;
-    const size_t lds = tx_lds > RK::LDS_BYTES ? tx_lds : RK::LDS_BYTES;
-    static_assert((size_t)2 * TK::PLANES + 256 * 4 <= (size_t)RK::TBL_OFF, "TX planes below the RX tap tables");
-    const void* k = reinterpret_cast<const void*>(&chain_flow<SPS, NKS_T, NKS_R, T, EM, LAG>);
-    ChainGeo g{};
-    if (!chain_flow_geo<SPS, NKS_T, NKS_R, T>(tp, rp, 1, g)) return hipErrorNotSupported;
-    const unsigned grid = persistent_grid(k, 256, lds, g.ntx);
-    hipLaunchKernelGGL((chain_flow<SPS, NKS_T, NKS_R, T, EM, LAG>), dim3(grid), dim3(256), lds, s, tp,
-                       static_cast<const th8*>(bfrag), rp, static_cast<const _Float16*>(tables), g);
-    return hipGetLastError();
-}
 
 template <int SPS, int NKS_T, int NKS_R, int EM>
 static hipError_t chain_small_go(const TxParams& tp, const void* bfrag, const RxParams& rp, const void* tables,
@@ -359,28 +265,6 @@ static hipError_t chain_go(const TxParams& tp, const void* bfrag, const RxParams
     }
 }
 
-// At size: the flow form (lag 0 or 1 round; f32, the steady-state epilogues). Both sides at
-// size (1024-symbol TX tiles, 1024-instant RX tiles).
-template <int SPS, int NKS_T, int NKS_R>
-static hipError_t chain_flow_go(const TxParams& tp, const void* bfrag, const RxParams& rp, const void* tables,
-                                hipStream_t s, int lag) {
-    if (tx_small_tiles(tp.nsym, 16 / SPS) || rx_small_tiles(rp.nout)) return hipErrorNotSupported;
-    auto go = [&](auto emc) -> hipError_t {
-        constexpr int E = decltype(emc)::value;
-        return lag == 0 ? chain_flow_em<SPS, NKS_T, NKS_R, float, E, 0>(tp, bfrag, rp, tables, s)
-                        : chain_flow_em<SPS, NKS_T, NKS_R, float, E, 1>(tp, bfrag, rp, tables, s);
-    };
-    switch (rx_mfma_em<float, MIX_COMPLEX, float>(rp)) {
-    case RXE_IQSYM: return go(std::integral_constant<int, RXE_IQSYM>());
-    default: return hipErrorNotSupported;
-    }
-}
-
-hipError_t launch_chain_flow(const TxParams& tp, int sps, int nks_t, const void* bfrag, const RxParams& rp,
-                             int nks_r, const void* tables, int dtype, hipStream_t s, int lag) {
-    if (dtype != 0 || sps != 4 || nks_t != 2 || nks_r != 6) return hipErrorNotSupported;   // C3
-    return chain_flow_go<4, 2, 6>(tp, bfrag, rp, tables, s, lag);
-}
 
 // (sps = decim, TX k-steps, RX k-steps): the BASELINE chains (C2/C4 QPSK 65 taps sps 4, C3
 // 129 taps sps 4, C5 513 taps sps 8); other filters run as the two launches.

@@ -155,10 +155,6 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
 // *form = 1 (chain_mfma) or 2 (chain_small: one RX tile per workgroup, LDS hand-off).
 hipError_t launch_chain_mfma(const TxParams& tp, int sps, int nks_t, const void* bfrag, const RxParams& rp,
                              int nks_r, const void* tables, int dtype, hipStream_t s, int* form);
-// The same period at size as one persistent launch of TX tiles each followed by an RX tile
-// (chain_flow: lag 0, the tile just written, or lag 1, the one written a round earlier).
-hipError_t launch_chain_flow(const TxParams& tp, int sps, int nks_t, const void* bfrag, const RxParams& rp,
-                             int nks_r, const void* tables, int dtype, hipStream_t s, int lag);
 hipError_t launch_fir(const FirParams& p, hipStream_t s);
 hipError_t launch_phases(float w, uint64_t s0, size_t n, float* out, hipStream_t s);
 hipError_t launch_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, hipStream_t s);

@@ -158,55 +158,3 @@ def test_fused_chain_one_output(m, o, torch_cuda, cfg, dtype, nsym, periods, whi
             assert torch.equal(s1[:k1], s2[:k2]), f"period {p}: decisions differ"
     assert all(h == form for h in how[1:]), how
     print(f"\n[fused one output] {cfg} {which}: forms {how}")
-
-
-# The flow form at size (modem_chain.hip chain_flow, MODEM_CHAIN_FLOW=1: lag 0, =2: lag 1 round):
-# (config, symbols per period, extra bits, periods, amplitude)
-FLOW_CASES = [
-    ("c3_qam16", 1 << 22, 0, 3, 1.0),           # the C3 call
-    ("c3_qam16", (1 << 22) - 4 * 1000 + 3, 1, 3, 1.0),   # ragged: leads change per period
-    ("c3_qam16", 1 << 21, 0, 2, 1.0 / 64),      # staged at a nonzero exponent
-]
-
-
-@pytest.mark.parametrize("flow", [1, 2])
-@pytest.mark.parametrize("cfg,nsym,extra,periods,amp", FLOW_CASES)
-def test_flow_chain_equals_two_launches(m, o, torch_cuda, cfg, nsym, extra, periods, amp, flow):
-    torch = torch_cuda
-    name, bps, L, sps = CONFIGS[cfg]
-    nb = nsym * bps + extra
-    hb = o.prng_bits(SEED + 500 + nsym % 1000, nb)
-    bits = torch.from_numpy(hb).cuda()
-    cap = (nb + bps) // bps * sps
-    bufs = []
-    for _ in range(2):
-        bufs.append((torch.empty((cap, 2), dtype=torch.float32, device="cuda"),
-                     torch.empty((cap // sps + 1, 2), dtype=torch.float32, device="cuda"),
-                     torch.empty(cap // sps + 1, dtype=torch.uint8, device="cuda")))
-    (txf, rxf), (txt, rxt) = make_pair(m, o, cfg, 0, amp), make_pair(m, o, cfg, 0, amp)
-    os.environ["MODEM_CHAIN_FLOW"] = str(flow)
-    try:
-        fl = m.ChainPlan(txf, rxf, bits, *bufs[0])
-    finally:
-        del os.environ["MODEM_CHAIN_FLOW"]
-    os.environ["MODEM_CHAIN_FUSED"] = "0"
-    try:
-        two = m.ChainPlan(txt, rxt, bits, *bufs[1])
-    finally:
-        del os.environ["MODEM_CHAIN_FUSED"]
-    how = []
-    for p in range(periods):
-        n1, k1 = fl.run()
-        n2, k2 = two.run()
-        torch.cuda.synchronize()
-        assert (n1, k1) == (n2, k2), p
-        how.append(fl.fused)
-        (y1, q1, s1), (y2, q2, s2) = bufs
-        assert torch.equal(y1[:n1], y2[:n2]), f"period {p}: samples differ"
-        assert torch.equal(q1[:k1], q2[:k2]), f"period {p}: RX I/Q differ"
-        assert torch.equal(s1[:k1], s2[:k2]), f"period {p}: decisions differ"
-        assert txf.carrier.sample == txt.carrier.sample and rxf.carrier.sample == rxt.carrier.sample
-    print(f"\n[flow {flow}] {cfg} nsym {nsym}+{extra}b amp {amp}: forms {how}")
-    # a stream's first period has no fused form (its first RX window reaches past TX tile 0)
-    if extra == 0:
-        assert all(h == 2 + flow for h in how[1:]), how
