@@ -664,9 +664,11 @@ struct RxMfma {
 
     // General path for tile t (all waves): two passes over its samples (max, then tile_ka
     // scale + split), the matched filter, the outputs in range. Returns its tile_ka.
-    template <int EM>
+    // HO (the fused small call): the window's samples of the call come from the LDS copy of
+    // what this workgroup's TX emitted (ho), not from HBM (the tail sub-tiles are only there).
+    template <int EM, bool HO = false>
     __device__ __forceinline__ static int slow_tile(const RxParams& p, _Float16* pl, const _Float16* tbl, float* reds, f32x4* part,
-                                    int64_t t, int kb, int ld) {
+                                    int64_t t, int kb, int ld, const RxHandoff& ho = RxHandoff{}) {
         // lane values recomputed here, not hoisted to the kernel entry (where, live across
         // the tile loop, they would spill)
         const int tid = tid_();
@@ -705,8 +707,16 @@ struct RxMfma {
             for (int k0 = 0; k0 < NK; k0 += BATCH) {
                 RawT v[BATCH];
 #pragma unroll
-                for (int b = 0; b < BATCH; ++b)       // < 0: wraps, out of range -> 0
-                    if (k0 + b < NK) v[b] = ld(rx, (uint32_t)(tid + (k0 + b) * NT - ox) * S);
+                for (int b = 0; b < BATCH; ++b) {     // < 0: wraps, out of range -> 0
+                    if (k0 + b >= NK) continue;
+                    if constexpr (HO) {                // (samples before the chunk: patched below)
+                        const int64_t i = q_lo + (tid + (k0 + b) * NT) - ho.base;
+                        const bool in = i >= 0 && i < ho.n && q_lo + (tid + (k0 + b) * NT) < p.N;
+                        v[b] = in ? ho.raw[i] : make_float2(0.f, 0.f);
+                    } else {
+                        v[b] = ld(rx, (uint32_t)(tid + (k0 + b) * NT - ox) * S);
+                    }
+                }
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int b = 0; b < BATCH; ++b) {
@@ -842,9 +852,9 @@ struct RxMfma {
     }
 
     // HO (the fused small call, modem_chain.hip): the tap tables are already in LDS, `ho.kin`
-    // holds *p.ka_in, and a first tile on the fast path reads its window from the LDS copy of
-    // the samples this workgroup's TX emitted (ho.raw) instead of from HBM; the general path,
-    // which reads HBM, first drains this workgroup's sample stores.
+    // holds *p.ka_in, and the tile reads its window from the LDS copy of the samples this
+    // workgroup's TX emitted (ho.raw) instead of from HBM, on the fast and the general path
+    // (samples before the call from the history, as always).
     template <int EM, bool HO = false>
     __device__ __forceinline__ static void run(const RxParams& p, _Float16* pl, _Float16* tbl, const _Float16* __restrict__ tables,
                                float* red, const TileSeq sq, int64_t bid, const RxHandoff& ho = RxHandoff{}) {
@@ -924,11 +934,7 @@ struct RxMfma {
             if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, part, w, cx, pre, kpred);
             else loop<true, EM>(p, pl, tbl, votes, part, w, cx, pre, kpred);
             if (w.i < w.count) {               // tile w.t on the general path (one place in the code)
-                if constexpr (HO) {            // it reads HBM: this workgroup's sample stores first
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
-                }
-                kpred = slow_tile<EM>(p, pl, tbl, reds, part, w.t, cx.kb, cx.ld);
+                kpred = slow_tile<EM, HO>(p, pl, tbl, reds, part, w.t, cx.kb, cx.ld, ho);
                 if (w.t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
                 w.next();
                 // reload the next tile (what the staging of tile i loaded is dropped: `pre` is

@@ -325,7 +325,8 @@ struct TxMfma {
 
     // Partial tile, samples before the call, or carrier index >= 2^53: guarded, 64-bit
     // indices; the same arithmetic as emit_full (a sample's bits never depend on the path).
-    template <bool RAW = false>
+    // STORE false: the LDS window only (a tail sub-tile its owner stores).
+    template <bool RAW = false, bool STORE = true>
     __device__ static void emit_edge(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale,
                                      const RawOut& ro = RawOut{}) {
         const int lane = threadIdx.x & 63;
@@ -344,8 +345,10 @@ struct TxMfma {
                 const int64_t i = jt + off - ro.base;
                 if (i >= 0 && i < ro.n) ro.p[i] = make_float2(z.x, z.y);
             }
-            if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, jt + off, z.x);
-            else OutIO<OutT>::store_one(p.out, jt + off, z.x, z.y);
+            if constexpr (STORE) {
+                if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, jt + off, z.x);
+                else OutIO<OutT>::store_one(p.out, jt + off, z.x, z.y);
+            }
         }
     }
 
@@ -373,7 +376,9 @@ struct TxMfma {
     // One tile t and, before it, the last xs sub-tiles of tile t - 1 (the fused small call,
     // modem_chain.hip: one RX tile per workgroup). The tail's symbol loads fly with the tile's
     // and the LUT's, both are staged before one barrier (the tail into the second plane set
-    // pl2), and (RAW) every emitted sample is also written to the LDS window `ro`.
+    // pl2), and (RAW) every emitted sample is also written to the LDS window `ro`. The tail's
+    // samples go to that window only: tile t - 1's workgroup stores them, and this workgroup's
+    // RX reads its whole window from LDS, on the general path too (RxMfma::slow_tile<HO>).
     template <int BPS, bool RAW = true>
     __device__ __forceinline__ static void one_tile(const TxParams& p, _Float16* pl, _Float16* pl2, th4* lut_s,
                                                     const th8 (&bh)[NKS], const th8 (&bl)[NKS], int64_t t, int xs,
@@ -440,7 +445,7 @@ struct TxMfma {
             if (tl && g >= g0) {                                    // wave-uniform
                 if (lv) fir<true>(pl2, q, bh, bl, dre, dim);
                 else fir<false>(pl2, q, bh, bl, dre, dim);
-                emit_edge<RAW>(p, j2 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
+                emit_edge<RAW, !RAW>(p, j2 + ((int64_t)g * 16 * SB) * SPS, dre, dim, unscale, ro);
             }
             if (lv) fir<true>(pl, q, bh, bl, dre, dim);
             else fir<false>(pl, q, bh, bl, dre, dim);
