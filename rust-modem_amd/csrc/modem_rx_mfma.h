@@ -328,6 +328,12 @@ struct RxMfma {
     static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
     static constexpr int NQ = (NS + 3) / 4;                     // quads
     static constexpr int U = (NQ + NT - 1) / NT;                // quads per lane
+    // K-split (C5): the tile's last, partial slot holds NS - 4 NT (U - 1) <= NT samples, staged one
+    // per lane (2 VGPRs for an f32 sample instead of a quad's 8: the quad form spilled 16 bytes
+    // at the tile loop's entry). UQ quads + that sample per lane.
+    static constexpr bool P1 = KS == 2 && NS - 4 * NT * (U - 1) <= NT;
+    static constexpr int UQ = P1 ? U - 1 : U;
+    using ST = typename std::conditional<std::is_same<InT, float>::value, float2, uint32_t>::type;
     // Plane layout. decim 4 and 8: unpadded, 16-B chunks XOR-swizzled within each row of
     // 8 (decim 4) or 16 (decim 8) chunks by the row bits — conflict-free A reads and staging
     // writes (tests/test_lds_banks.py) and no pad halves, which lets 4 workgroups share a CU
@@ -436,6 +442,19 @@ struct RxMfma {
         constexpr int S = sizeof(InT) * 2;
         const uint32_t w = clamp64_u32(p.N - q_lo, (uint32_t)(4 * NQ));
         return buf_rsrc(reinterpret_cast<const char*>(p.x) + q_lo * S, live ? w * (uint32_t)S : 0u);
+    }
+    // P1: lane tid's sample of the partial slot (window sample 4 NT (U - 1) + tid)
+    __device__ static ST load_one(__amdgpu_buffer_rsrc_t r, int tid) {
+        constexpr int S = sizeof(InT) * 2;
+        const int o = (4 * NT * (U - 1) + tid) * S;
+        if constexpr (std::is_same<InT, float>::value)
+            return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0));
+        else
+            return __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0);
+    }
+    __device__ static float2 one_f2(const ST& v) {
+        if constexpr (std::is_same<InT, float>::value) return v;
+        else return __half22float2(__builtin_bit_cast(__half2, v));
     }
     __device__ static QT load_slot(__amdgpu_buffer_rsrc_t r, int voff, int u) {
         constexpr int S = sizeof(InT) * 2;
@@ -567,7 +586,7 @@ struct RxMfma {
     // (`nxt`). Each wave writes its three votes (max >= window lo, >= window hi, normal).
     template <bool SC>
     __device__ static void stage(const RxParams& p, _Float16* pl, int* vote, Idx ix, float sc, cf2 win,
-                                 QT (&pre)[U], __amdgpu_buffer_rsrc_t nxt) {
+                                 QT (&pre)[UQ], ST& ps, __amdgpu_buffer_rsrc_t nxt) {
         const int tid = tid_();
         int pos0 = ppos(4 * tid);
         int voff = 4 * tid * (int)sizeof(InT) * 2;
@@ -577,7 +596,7 @@ struct RxMfma {
         const float roff = p.phase_offset * kRcp2Pi;          // rx_sincos: carrier + PLL offset, in turns
         float mx = 0.f;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < UQ; ++u) {
             if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) {   // partial last slot: not this wave's
                 pre[u] = load_slot(nxt, voff, u);
                 continue;
@@ -610,6 +629,27 @@ struct RxMfma {
             __builtin_amdgcn_sched_barrier(0);
             pre[u] = load_slot(nxt, voff, u);                  // the next tile's slot u, same registers
             __builtin_amdgcn_sched_barrier(0);                 // one quad's temporaries at a time
+        }
+        if constexpr (P1) {                    // the partial slot, one sample per lane: the quad path's
+            const int e = 4 * NT * (U - 1) + tid;               // arithmetic for sample e, bit for bit
+            if (e < NS) {
+                const float2 x = one_f2(ps);
+                const float nf = (bl + (float)(4 * NT * (U - 1) - 3 * tid)) + ix.a;   // (b + e) exact, one rounding
+                const float rv = __builtin_fmaf(phase_from_f2(p.w, (cf2){nf, nf}).x, kRcp2Pi, roff);
+                const float sn = __builtin_amdgcn_sinf(rv), cs = __builtin_amdgcn_cosf(rv);
+                cf2 z = MIX == MIX_REFERENCE_REAL ? (cf2){x.x * cs, x.x * -sn} : cmix((cf2){x.x, x.y}, (cf2){cs, sn});
+                if (SC) z = z * sc;
+                asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(z.x), "v"(z.y));
+                h2 hi, lo;
+                split2(z, hi, lo);
+                const int o = ppos(e);
+                pl[o] = hi.x;
+                pl[PL + o] = lo.x;
+                pl[2 * PL + o] = hi.y;
+                pl[3 * PL + o] = lo.y;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            ps = load_one(nxt, tid);
         }
         // three votes per wave instead of a max reduction
         const bool blo = __ballot(mx >= win.x) != 0, bhi = __ballot(mx >= win.y) != 0,
@@ -827,7 +867,7 @@ struct RxMfma {
     // at the end of the walk, or after the barrier of a tile the general path must redo.
     template <bool SC, int EM>
     __device__ __forceinline__ static void loop(const RxParams& p, _Float16* pl, const _Float16* tbl, int* votes, f32x4* part,
-                                Walk& w, const Ctx& cx, QT (&pre)[U], int kpred) {
+                                Walk& w, const Ctx& cx, QT (&pre)[UQ], ST& ps, int kpred) {
         const float sc = __builtin_ldexpf(1.0f, kpred);
         const cf2 win = window(kpred);
         while (w.i < w.count) {
@@ -840,7 +880,7 @@ struct RxMfma {
             // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
             // event, +0.8 % bench (profiles/r02_store_layout_ab.txt; priority 3: no better)
             __builtin_amdgcn_s_setprio(1);
-            stage<SC>(p, pl, votes, ix, sc, win, pre, nxt);
+            stage<SC>(p, pl, votes, ix, sc, win, pre, ps, nxt);
             __builtin_amdgcn_s_setprio(0);
             __syncthreads();
             if (!(fi && fast_ok(votes, kpred))) return;
@@ -864,12 +904,14 @@ struct RxMfma {
         int* votes = reinterpret_cast<int*>(red);            // [NW]
         float* reds = red + NW;                              // [NW]
         f32x4* part = reinterpret_cast<f32x4*>(red + 2 * NW);   // KS = 2: [2][NWF][64]
-        QT pre[U];
+        QT pre[UQ];
+        ST ps{};                                             // P1: the partial slot's sample
         auto prefetch = [&](int64_t q, bool live) {
             const __amdgpu_buffer_rsrc_t r = window_rsrc(p, live ? q : 0, live);
             const int voff = 4 * tid_() * (int)sizeof(InT) * 2;
 #pragma unroll
-            for (int u = 0; u < U; ++u) pre[u] = load_slot(r, voff, u);
+            for (int u = 0; u < UQ; ++u) pre[u] = load_slot(r, voff, u);
+            if constexpr (P1) ps = load_one(r, tid_());
         };
         // the tap tables into LDS, their loads issued before the first tile's so that the two
         // memory latencies at the kernel's start overlap (the table stores wait for the table
@@ -878,13 +920,14 @@ struct RxMfma {
         const bool f0 = w.full();
         if constexpr (HO) {
             static_assert(std::is_same<InT, float>::value, "LDS hand-off: f32 samples");
+            static_assert(!P1, "LDS hand-off: quad slots");
             if (!f0) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) pre[u] = QT{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+                for (int u = 0; u < UQ; ++u) pre[u] = QT{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
             } else {                           // the window from the LDS copy (zeros past it and the call)
                 const int e = 4 * tid_();
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
+                for (int u = 0; u < UQ; ++u) {
                     float2 x[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -915,8 +958,12 @@ struct RxMfma {
         int kpred = kin >= -120 && kin <= 120 && (kin & 7) == 0 ? kin : 0;
         if (f0 && kin == INT32_MIN) {          // a stream's first call: from the first tile's raw input
             float mx = 0.f;
+            if constexpr (P1) {                // (zeros past the window)
+                const float2 x = one_f2(ps);
+                asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(x.x), "v"(x.y));
+            }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
+            for (int u = 0; u < UQ; ++u) {
                 if ((u + 1) * NT > NQ && 64 * wave + NT * u >= NQ) continue;
                 float2 x[4];
                 Q::split(pre[u], x);
@@ -931,8 +978,8 @@ struct RxMfma {
             __syncthreads();
         }
         while (w.i < w.count) {
-            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, part, w, cx, pre, kpred);
-            else loop<true, EM>(p, pl, tbl, votes, part, w, cx, pre, kpred);
+            if (kpred == 0) loop<false, EM>(p, pl, tbl, votes, part, w, cx, pre, ps, kpred);
+            else loop<true, EM>(p, pl, tbl, votes, part, w, cx, pre, ps, kpred);
             if (w.i < w.count) {               // tile w.t on the general path (one place in the code)
                 kpred = slow_tile<EM, HO>(p, pl, tbl, reds, part, w.t, cx.kb, cx.ld, ho);
                 if (w.t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
