@@ -328,10 +328,11 @@ struct RxMfma {
     static constexpr int NS = (TS - 16) * DEC + W;              // samples staged per tile
     static constexpr int NQ = (NS + 3) / 4;                     // quads
     static constexpr int U = (NQ + NT - 1) / NT;                // quads per lane
-    // K-split (C5): the tile's last, partial slot holds NS - 4 NT (U - 1) <= NT samples, staged one
-    // per lane (2 VGPRs for an f32 sample instead of a quad's 8: the quad form spilled 16 bytes
-    // at the tile loop's entry). UQ quads + that sample per lane.
-    static constexpr bool P1 = KS == 2 && NS - 4 * NT * (U - 1) <= NT;
+    // 1024-instant tiles: the tile's last, partial slot holds NS - 4 NT (U - 1) <= NT samples
+    // (C3: 128, C5: 512), staged one per lane (2 VGPRs for an f32 sample instead of a quad's 8:
+    // the quad form spilled 16 bytes in C5's K-split kernel; at C3 the 6 VGPRs freed for the
+    // matched filter took the RX 29.80 -> 29.54 us). UQ quads + that sample per lane.
+    static constexpr bool P1 = NWF == 4 && NS - 4 * NT * (U - 1) <= NT;
     static constexpr int UQ = P1 ? U - 1 : U;
     using ST = typename std::conditional<std::is_same<InT, float>::value, float2, uint32_t>::type;
     // Plane layout. decim 4 and 8: unpadded, 16-B chunks XOR-swizzled within each row of
