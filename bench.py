@@ -6,8 +6,10 @@ A step is one pass of the hot path over one batch: bits (device-resident, one by
 -> RX kernel (conjugate mix + matched filter at the symbol instants + slicer) -> decimated
 I/Q + u8 decisions. Workload per GPU is BASELINE config 3 (16-QAM, 129-tap RRC, sps 4,
 16 M samples); with --gpus N each rank runs its own independent channel (weak scaling, no
-data-path collective — SURVEY.md §8e). `value` = samples processed by all ranks / the max
-over ranks of the timed region. Before the warmup each rank runs --settle-ms (300) of untimed
+data-path collective — SURVEY.md §8e). `--config c4` is BASELINE config 4 as the one job it
+names: 64 QPSK channels of 2^22 samples over the node, 64 / N per GPU (strong scaling), each
+step running the rank's channels in groups of 8 (a TX launch, then an RX launch, per group).
+`value` = samples processed by all ranks / the max over ranks of the timed region. Before the warmup each rank runs --settle-ms (300) of untimed
 back-to-back steps: the device clock dips for the first ~100 ms of sustained load, and the
 driver's 20-step region (~1.2 ms) would otherwise measure that transient (tools/region_probe.py).
 
@@ -39,11 +41,32 @@ WORKLOADS = {
     "c3": ("qam16", 4, 129, 4, 1 << 24, 1, 0,
            "c3: 16-QAM, 129-tap RRC TX + matched-filter RX loopback, 2^24 complex f32 samples/GPU"),
     "c2": ("qpsk", 2, 65, 4, 1 << 20, 1, 0, "c2: QPSK, 65-tap RRC, 2^20 complex f32 samples/GPU"),
-    "c4": ("qpsk", 2, 65, 4, 1 << 22, 8, 0,
-           "c4: 8 independent QPSK channels x 2^22 complex f32 samples per GPU, 65-tap RRC"),
+    "c4": ("qpsk", 2, 65, 4, 1 << 22, 64, 0,
+           "c4: 64 independent QPSK channels x 2^22 complex f32 samples over the node (64/N per GPU), 65-tap RRC"),
     "c5": ("qam256", 8, 513, 8, 1 << 26, 1, 0, "c5: 256-QAM, 513-tap RRC, sps 8, 2^26 complex f32 samples/GPU"),
     "c5h": ("qam256", 8, 513, 8, 1 << 26, 1, 1, "c5: 256-QAM, 513-tap RRC, sps 8, 2^26 complex f16 samples/GPU"),
 }
+
+# BASELINE config 4 is one fixed job, "64 independent QPSK channels x 4 M samples, sharded 8 per
+# GPU across 8 x MI355X": its channel count is the whole node's, and --gpus N gives each rank
+# 64 / N of them (strong scaling: the 1-, 2-, 4- and 8-GPU lines time the same 2^28 samples).
+# Every other config's count is per GPU (weak scaling).
+FIXED_TOTAL = {"c4"}
+# channels per TX / RX launch pair of a multi-channel step (the batch entry points take up to 8
+# per launch, modem_internal.h kBatchMax); the groups run one after another, TX then RX each
+GROUP_DEFAULT = {"c4": 8}
+
+
+def rank_workload(config, world):
+    """The workload tuple one rank runs and the line's scaling: for FIXED_TOTAL configs the
+    channel count becomes count / world (it must divide), else it is already per GPU."""
+    wl = WORKLOADS[config]
+    if config not in FIXED_TOTAL:
+        return wl, "weak"
+    total = wl[5]
+    if world < 1 or total % world:
+        raise ValueError(f"config {config}: {total} channels do not split over {world} GPUs")
+    return wl[:5] + (total // world,) + wl[6:], "strong"
 
 
 def algorithmic_bytes(bps, ntaps, sps, nsamp, dtype):
@@ -57,14 +80,16 @@ def algorithmic_bytes(bps, ntaps, sps, nsamp, dtype):
 
 
 def channel_seed(rank, nch, c):
-    """Channel c of rank `rank`: every rank owns distinct channels (weak scaling, no exchange)."""
+    """Channel c of rank `rank` (nch channels per rank) is global channel rank * nch + c: every
+    rank owns distinct channels (no exchange), and a FIXED_TOTAL job's ranks cover exactly its
+    channels 0 .. total - 1, whatever the node size."""
     return SEED + rank * nch + c
 
 
 class GpuRunner:
     """The product path: rust_modem_amd handles on this rank's GPU, buffers resident in HBM."""
 
-    def __init__(self, wl, rank, device, streams=1, batch=False, amplitude=1.0):
+    def __init__(self, wl, rank, device, streams=1, batch=False, amplitude=1.0, group=0):
         import torch
         import __graft_entry__ as g
         self.torch = torch
@@ -104,10 +129,17 @@ class GpuRunner:
             osym = torch.empty(nsamp // sps, dtype=torch.uint8, device=f"cuda:{device}")
             self.ch.append(dict(bits=bits, tx=tx, rx=rx, y=y, oiq=oiq, osym=osym, nout=nout))
         if batch:       # prepared batch calls over the fixed per-channel buffers
-            ch = self.ch
-            self._txp = m.TxBatchPlan([d["tx"] for d in ch], [d["bits"] for d in ch], [d["y"] for d in ch])
-            self._rxp = m.RxBatchPlan([d["rx"] for d in ch], [d["y"] for d in ch], [d["oiq"] for d in ch],
-                                      [d["osym"] for d in ch])
+            # groups of `group` channels (all of them when 0): the step runs each group's TX
+            # launch and then its RX launch, so that a group's samples are re-read while they
+            # are still in the Infinity Cache (64 channels x 32 MiB at once would not be)
+            g = group if group > 0 else nch
+            self.group = min(g, nch)
+            self._txp, self._rxp = [], []
+            for c0 in range(0, nch, self.group):
+                ch = self.ch[c0:c0 + self.group]
+                self._txp.append(m.TxBatchPlan([d["tx"] for d in ch], [d["bits"] for d in ch], [d["y"] for d in ch]))
+                self._rxp.append(m.RxBatchPlan([d["rx"] for d in ch], [d["y"] for d in ch], [d["oiq"] for d in ch],
+                                               [d["osym"] for d in ch]))
         # one prepared C call per channel and step (modem_chain_run = modem_tx_process +
         # modem_rx_process on the fixed device buffers): the TX and RX kernels of the step with
         # the buffers checked once, so that the host stays ahead of small steps (C2)
@@ -126,8 +158,9 @@ class GpuRunner:
 
     def step(self):
         if self.batch:
-            self._txp.run()
-            self._rxp.run()
+            for txp, rxp in zip(self._txp, self._rxp):
+                txp.run()
+                rxp.run()
             return
         if len(self.streams) == 1 and self._plans:
             for pl in self._plans:
@@ -196,15 +229,20 @@ class GpuRunner:
             res.append(ev[0].elapsed_time(ev[1]) / n)
         return sorted(res)[rounds // 2]
 
+    def launch_channels(self):
+        """Channels one timed TX or RX launch covers (the legs time the first group)."""
+        return self.group if self.batch else 1
+
     def _tx_all(self):
         if self.batch:
-            self._txp.run()
+            self._txp[0].run()
         else:
             self.tx(0)
 
     def _step_timed(self):
         if self.batch:
-            self.step()
+            self._txp[0].run()
+            self._rxp[0].run()
         elif self._plans:
             self._plans[0].run()
         else:
@@ -213,14 +251,13 @@ class GpuRunner:
 
     def _rx_all(self):
         if self.batch:
-            self._rxp.run()
+            self._rxp[0].run()
         else:
             self.rx(0)
 
     def kernel_times_ms(self, budget_ms=10.0, min_reps=200, rounds=5):
-        """Mean device time of one TX launch, one RX launch and one TX+RX step, from HIP events
-        on the launch stream (channel 0's launches, or the batch launches that cover every
-        channel). Each leg is timed directly as back-to-back launches between two events: TX
+        """Mean device time of one TX launch, one RX launch and one TX+RX pair, from HIP events
+        on the launch stream (channel 0's launches, or the first channel group's batch launches). Each leg is timed directly as back-to-back launches between two events: TX
         alone, RX alone (re-reading the sample buffer the last TX wrote, resident in HBM), and
         the chain. The amount of work is a device-time budget, independent of --steps (the
         driver's 20 steps are ~1 ms of C3, while the clock settles over the first few ms of
@@ -377,7 +414,7 @@ def pmc_traffic(config):
 
 
 def run(args, runner_factory, dist=None, rank=0, world=1):
-    wl = WORKLOADS[args.config]
+    wl, scaling = rank_workload(args.config, world)
     name, bps, L, sps, nsamp, nch, dtype, desc = wl
     r = runner_factory(wl, rank)
     # Clock settling (untimed): back-to-back steps for --settle-ms of wall time before the
@@ -414,7 +451,7 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
         g_ms = dist.max_over_ranks(g_ms)
     t_tx, t_rx, t_chain = r.kernel_times_ms()
     b_tx, b_rx, nout = algorithmic_bytes(bps, L, sps, nsamp, dtype)
-    per_launch = nch if getattr(r, "batch", False) else 1      # channels one timed launch covers
+    per_launch = r.launch_channels() if hasattr(r, "launch_channels") else 1   # channels one timed launch covers
     b_tx, b_rx, nsamp_launch = b_tx * per_launch, b_rx * per_launch, nsamp * per_launch
     # the step's kernels: one fused launch (small calls, modem_chain.hip) or the TX and RX
     # launches, of which the longer is the dominant kernel
@@ -456,16 +493,18 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
         "settle": settle,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f16" if dtype == 1 else "f32",
         "data": f"synthetic: splitmix64 bits (seed 0x5EED0000 + channel), one byte per bit, device-resident",
         "config": {"workload": desc, "samples_per_gpu_per_step": nsamp * nch, "channels_per_gpu": nch,
+                   "channels_total": nch * world, "channels_per_launch": per_launch,
                    "streams_per_gpu": len(getattr(r, "streams", [None])),
                    "channel_batch": bool(getattr(r, "batch", False)),
                    "ntaps": L, "sps": sps, "bits_per_symbol": bps, "rrc_beta": 0.35,
                    "carrier": "Freq::new(1, 4) (fs/4)", "parallelism": f"{world} independent channel set(s), "
-                   "one per GPU, no collectives" + (f" (timing barrier and max over ranks: "
+                   "one per GPU, no collectives" + (f"; one job of {nch * world} channels, {nch} per GPU"
+                                                    if scaling == "strong" else "") + (f" (timing barrier and max over ranks: "
                                                     f"{dist.td.get_backend()})" if dist is not None else "")},
         "roofline": {"bound": "hbm", "kernel": dom[0], "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": dom_traffic,
@@ -588,6 +627,8 @@ def _parser():
     # multi-channel configs go through modem_*_process_batch (one launch for all channels of
     # the step) unless --no-batch, which queues per-channel calls on --streams streams
     ap.add_argument("--no-batch", action="store_true")
+    # channels per TX / RX launch pair of a batched step (0: the config's default, GROUP_DEFAULT)
+    ap.add_argument("--group", type=int, default=0)
     # constellation amplitude (1.0 = BASELINE); e.g. 1/16 puts the RX input below 2^-3
     ap.add_argument("--amplitude", type=float, default=1.0)
     # skip the C5 f32 out-of-Infinity-Cache roofline measured after the C3 line
@@ -681,6 +722,11 @@ def main(argv=None):
     args = _parser().parse_args(argv)
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
+    try:
+        rank_workload(args.config, args.gpus)
+    except ValueError as e:               # before any GPU work: a node size the job does not split over
+        print(f"bench.py: {e}", file=sys.stderr)
+        raise SystemExit(2)
     wenv = os.environ.get("WORLD_SIZE")
     if wenv is None and args.gpus > 1:
         return _spawn(args, argv)
@@ -689,6 +735,7 @@ def main(argv=None):
         print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world} of the launcher",
               file=sys.stderr)
         raise SystemExit(2)
+    wl, _ = rank_workload(args.config, world)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -707,10 +754,11 @@ def main(argv=None):
         else:                 # ranks share a GPU (a one-GPU box): RCCL cannot, gloo on the host
             td.init_process_group("gloo")
             dist = _Dist(td, None)
-    nch = WORKLOADS[args.config][5]
+    nch = wl[5]
     nst = args.streams if args.streams > 0 else min(nch, 4)
     batch = nch > 1 and not args.no_batch
-    out = run(args, lambda wl, r: GpuRunner(wl, r, device, 1 if batch else nst, batch, args.amplitude),
+    group = args.group if args.group > 0 else GROUP_DEFAULT.get(args.config, 0)
+    out = run(args, lambda wl, r: GpuRunner(wl, r, device, 1 if batch else nst, batch, args.amplitude, group),
               dist, rank, world)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -577,7 +577,8 @@ static int64_t tx_nt_below(int64_t nsamp, uint64_t launch_bytes, bool single) {
     static const int mode = [] { const char* e = std::getenv("MODEM_TX_NT"); return e ? std::atoi(e) : 2; }();
     constexpr uint64_t kMin = 192ull << 20, kCache = 256ull << 20;
     if (mode == 0 || launch_bytes <= kMin || nsamp <= 0) return 0;
-    return mode == 2 && single && launch_bytes <= kCache ? nsamp / 2 : nsamp;
+    // the cacheable second half pays only because the RX reads it first (mk::kRxTilesTopDown)
+    return mode == 2 && single && mk::kRxTilesTopDown && launch_bytes <= kCache ? nsamp / 2 : nsamp;
 }
 
 // Kernel parameters of one TX call on device buffers (dbits, dout); see tx_run.

@@ -7,6 +7,12 @@
 
 namespace mk {
 
+// The RX MFMA kernels walk a call's tiles in rounds from the top down (rx_mfma_body), so the
+// last samples a TX launch wrote are the first the RX reads. The TX store policy relies on it
+// (modem_capi.cpp tx_nt_below: a single-channel launch of <= 256 MiB keeps its second half
+// cacheable); rx_mfma_body asserts it. Changing the RX walk means revisiting that policy.
+constexpr bool kRxTilesTopDown = true;
+
 // One TX launch: symbols [0, nsym) of this call -> samples [0, nsym*sps).
 struct TxParams {
     const uint8_t* bits;     // this call's bits, one byte per bit (device)

@@ -641,13 +641,19 @@ struct RxMfma {
                 cf2 z = MIX == MIX_REFERENCE_REAL ? (cf2){x.x * cs, x.x * -sn} : cmix((cf2){x.x, x.y}, (cf2){cs, sn});
                 if (SC) z = z * sc;
                 asm("v_max3_f32 %0, %0, |%1|, |%2|" : "+v"(mx) : "v"(z.x), "v"(z.y));
-                h2 hi, lo;
-                split2(z, hi, lo);
                 const int o = ppos(e);
-                pl[o] = hi.x;
-                pl[PL + o] = lo.x;
-                pl[2 * PL + o] = hi.y;
-                pl[3 * PL + o] = lo.y;
+                if constexpr (HI) {            // two planes, the f16 roundings only (as put4)
+                    const h2 h = __builtin_convertvector(z, h2);
+                    pl[o] = h.x;
+                    pl[PL + o] = h.y;
+                } else {
+                    h2 hi, lo;
+                    split2(z, hi, lo);
+                    pl[o] = hi.x;
+                    pl[PL + o] = lo.x;
+                    pl[2 * PL + o] = hi.y;
+                    pl[3 * PL + o] = lo.y;
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
             ps = load_one(nxt, tid);
@@ -1015,6 +1021,7 @@ __device__ __forceinline__ void rx_mfma_body(const RxParams& p, const _Float16* 
         if (bid == 0 && threadIdx.x == 0) *p.ka_out = *p.ka_in;
         return;
     }
+    static_assert(kRxTilesTopDown, "the TX store policy (tx_nt_below) assumes the top-down walk");
     const int64_t R = (ntiles + nb - 1) / nb * nb;
     TileSeq sq{R - nb + bid, -nb, R / nb, ntiles};
     if (sq.first >= ntiles) { sq.first -= nb; --sq.count; }

@@ -289,11 +289,15 @@ struct TxMfma {
         const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
         char* ob = reinterpret_cast<char*>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(oa >> 32)) << 32) |
                                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)oa));
-        if constexpr (std::is_same<OutT, __half>::value && OUT_MODE != OUT_REAL) {
-            // f16 samples (4 B): a lane's one-sample stores would leave every 16-lane group
-            // writing half a 128-B line. Neighbour lanes swap one packed sample (DPP) so that the
-            // even lane holds samples i, i+1 of row r and the odd one samples i-1, i of row r+1:
-            // each 8-B store instruction then writes rows r and r+1 of the group, one whole line.
+        // f16 samples (4 B): a lane's one-sample stores would leave every 16-lane group
+        // writing half a 128-B line. Neighbour lanes swap one packed sample (DPP) so that the
+        // even lane holds samples i, i+1 of row r and the odd one samples i-1, i of row r+1:
+        // each 8-B store instruction then writes rows r and r+1 of the group, one whole line.
+        // Every such store lands at oa + 8 k, so the form needs oa 8-byte aligned (uniform); a
+        // caller's f16 buffer that is only 4-byte aligned (a sliced (n, 2) tensor) or a
+        // sub-tile at an odd call sample takes the one-sample stores below.
+        if (std::is_same<OutT, __half>::value && OUT_MODE != OUT_REAL && (oa & 7) == 0) {
+            typedef uint32_t u2v __attribute__((ext_vector_type(2)));
             const bool odd = lane & 1;
 #pragma unroll
             for (int r = 0; r < 4; r += 2) {
@@ -303,7 +307,6 @@ struct TxMfma {
                 const uint2 v = odd ? make_uint2(recv, b) : make_uint2(a, recv);
                 char* q = ob + (uint32_t)((odd ? loff + 16 * (r + 1) - 1 : loff + 16 * r) * SBYTES);
                 if (jt < p.nt_below) {          // uniform: past the Infinity Cache (tx_nt_below)
-                    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
                     __builtin_nontemporal_store((u2v){v.x, v.y}, reinterpret_cast<u2v*>(q));
                 } else {
                     *reinterpret_cast<uint2*>(q) = v;

@@ -67,7 +67,7 @@ class CpuRunner:
         return True
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, config="tiny"):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -76,7 +76,10 @@ def _worker(rank, world, port, outdir):
     import oracle as o
     td.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     bench.WORKLOADS["tiny"] = ("qam16", 4, 129, 4, 1 << 12, 2, 0, "tiny: 2 channels x 4096 samples")
-    args = bench.argparse.Namespace(config="tiny", steps=3, warmup=1, no_cpu_baseline=True, cpu_samples=0,
+    # a fixed job of 4 channels over the node (as config 4's 64): 4 / world per rank
+    bench.WORKLOADS["tinyjob"] = ("qam16", 4, 129, 4, 1 << 12, 4, 0, "tinyjob: 4 channels x 4096 samples")
+    bench.FIXED_TOTAL.add("tinyjob")
+    args = bench.argparse.Namespace(config=config, steps=3, warmup=1, no_cpu_baseline=True, cpu_samples=0,
                                     amplitude=1.0, no_out_of_cache=True, settle_ms=0.0)
     runners = []
 
@@ -111,6 +114,39 @@ def test_two_ranks_gloo(tmp_path):
         g = out["gather"]
         assert g["bytes_per_gpu"] == 2 * (((1 << 12) - 128) // 4) and g["ms"] >= 0   # L - 1 = 128 samples of lag
     assert outs[0]["gather"]["ms"] == outs[1]["gather"]["ms"]
+
+
+def test_fixed_job_splits_channels_over_ranks(tmp_path):
+    """A FIXED_TOTAL config (config 4: 64 channels over the node) at world size 2: each rank runs
+    half of the job's channels, the ranks' seeds are exactly global channels 0 .. total - 1 with
+    no overlap, `value` counts the whole job once, and the line says strong scaling."""
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "tinyjob"), nprocs=world, join=True)
+    outs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+    import bench
+    for out in outs:
+        assert out["scaling"] == "strong" and out["decisions_match_sent"] is True
+        assert out["config"]["channels_per_gpu"] == 2 and out["config"]["channels_total"] == 4
+    seeds = outs[0]["_seeds"] + outs[1]["_seeds"]
+    assert sorted(seeds) == [bench.SEED + c for c in range(4)]
+    total = (1 << 12) * 4 * 3
+    assert abs(outs[0]["value"] - total / (outs[0]["ms_per_step"] * 3 / 1e3) / 1e6) <= 0.02 * outs[0]["value"]
+
+
+def test_fixed_job_rank_workload():
+    """bench.rank_workload: config 4's 64 channels split 64 / 32 / 16 / 8 over 1 / 2 / 4 / 8 GPUs;
+    a node size that does not divide the job is refused (bench.py exits 2 before any GPU work);
+    the other configs keep their per-GPU count (weak scaling)."""
+    import bench
+    for n in (1, 2, 4, 8):
+        wl, sc = bench.rank_workload("c4", n)
+        assert wl[5] == 64 // n and sc == "strong" and wl[4] == 1 << 22
+    assert bench.rank_workload("c3", 8) == (bench.WORKLOADS["c3"], "weak")
+    with pytest.raises(ValueError):
+        bench.rank_workload("c4", 3)
+    with pytest.raises(SystemExit) as e:
+        bench.main(["--gpus", "3", "--config", "c4"])
+    assert e.value.code == 2
 
 
 def test_gpus_flag_must_match_launcher(monkeypatch):

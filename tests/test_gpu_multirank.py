@@ -60,19 +60,37 @@ def test_two_ranks_real_kernels(tmp_path):
 
 def test_bench_gpus_flag_two_ranks():
     """`bench.py --gpus 2` without a launcher: two fresh rank processes (here both on the box's
-    one GPU, so the timing barrier runs over gloo; one GPU per rank uses RCCL), each running
-    config 4's 8-channel workload; rank 0's line reports the node size, every channel's
-    decisions on both ranks, and the host gather of the decisions timed apart from `value`."""
+    one GPU, so the timing barrier runs over gloo; one GPU per rank uses RCCL) sharing config 4's
+    one 64-channel job, 32 channels each in groups of 8; rank 0's line reports the node size,
+    every channel's decisions on both ranks, and the host gather of the decisions timed apart
+    from `value`, which counts the job's 64 x 2^22 samples per step."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
-    out = bench.main(["--gpus", "2", "--config", "c4", "--steps", "10", "--warmup", "3", "--no-cpu-baseline"])
-    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
+    out = bench.main(["--gpus", "2", "--config", "c4", "--steps", "10", "--warmup", "3", "--settle-ms", "50",
+                      "--no-cpu-baseline"])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert out["config"]["channels_per_gpu"] == 32 and out["config"]["channels_total"] == 64
+    assert out["config"]["channels_per_launch"] == 8
     assert out["decisions_match_sent"] is True
     g = out["gather"]
-    assert g["bytes_per_gpu"] == 8 * ((1 << 22) // 4 - 16) and g["ms"] > 0
-    total = (1 << 22) * 8 * 10 * 2
+    assert g["bytes_per_gpu"] == 32 * ((1 << 22) // 4 - 16) and g["ms"] > 0
+    total = (1 << 22) * 64 * 10
     assert abs(out["value"] - total / (out["ms_per_step"] * 10 / 1e3) / 1e6) <= 0.02 * out["value"]
+
+
+def test_c4_job_one_gpu_groups_of_four():
+    """Config 4's whole 64-channel job on one GPU (the N = 1 point of its scaling curve), in
+    groups of 4 channels per launch pair: every channel's decisions equal the symbols it sent."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    out = bench.main(["--config", "c4", "--group", "4", "--steps", "5", "--warmup", "2", "--settle-ms", "20",
+                      "--no-cpu-baseline"])
+    assert out["n_gpus"] == 1 and out["scaling"] == "strong"
+    assert out["config"]["channels_per_gpu"] == 64 and out["config"]["channels_per_launch"] == 4
+    assert out["decisions_match_sent"] is True
+    assert out["gather"]["bytes_per_gpu"] == 64 * ((1 << 22) // 4 - 16)
 
 
 def test_rccl_branch_under_launcher(tmp_path):

@@ -168,6 +168,32 @@ def test_c5_prefix_against_oracle(m, o, torch_cuda, dtype):
     assert np.array_equal(host(gsym), sent_symbols(bits, bps)[: len(rsym)])
 
 
+@pytest.mark.parametrize("sps,L,phasor", [(4, 129, "c3_qam16"), (4, 65, "c2_qpsk"), (2, 129, "c3_qam16")])
+def test_rx_f16_large_tiles_against_oracle(m, o, torch_cuda, sps, L, phasor):
+    """f16 samples in and out of the RX on its 1024-instant tiles (>= 4 tiles per CU) at decim 4
+    (129 and 65 taps) and decim 2 (129 taps): the tile's partial last staging slot is staged one
+    sample per lane into the two f16 planes. I/Q within 2^-10 of the oracle's max (the oracle
+    reads the same f16-rounded input), decisions bit-exact to the oracle and the symbols sent."""
+    torch = torch_cuda
+    name, bps, _, _ = CONFIGS[phasor]
+    ninst = (4 * 1024 * 256) + 3 * 1024 + 77            # past rx_small_tiles on 256 CUs, ragged end
+    nsym = ninst + (L - 1) // sps + 1
+    bits = o.prng_bits(SEED + 7 + sps + L, nsym * bps)
+    taps = o.rrc_taps(L, sps, 0.35)
+    w = o.sample_freq(1, 4)
+    x = o.tx_chain(oracle_phasor(o, name), bits, sps, taps, w, 0).astype(np.float16)
+    xin = x.astype(np.float32)
+    riq, rsym = o.rx_chain(xin, w, 0, o.MIX_COMPLEX, taps, sps, L - 1, oracle_slicer(o, name, bps))
+    rx = m.DemodulatorRx(m.Carrier(w), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                         slicer=product_phasor(m, name).slicer(), in_dtype=1, out_dtype=1)
+    giq, gsym = rx.process(torch.from_numpy(x).cuda())
+    giq, gsym = host(giq).astype(np.float32), host(gsym)
+    assert giq.shape == riq.shape and len(rsym) >= 4 * 1024 * 256
+    report(f"RX f16->f16 decim {sps} {L} taps, {len(rsym)} instants", rel_err(giq, riq), 2.0 ** -10)
+    assert np.array_equal(gsym, rsym)
+    assert np.array_equal(gsym, sent_symbols(bits, bps)[: len(gsym)])
+
+
 def test_rx_streaming_across_scales_equals_one_call(m, o, torch_cuda, c3_stream):
     """A stream whose amplitude jumps between 2^-20 and 2^12 in segments, cut into calls of
     ragged sizes (many tiles per call; each call's first exponent is predicted from where the
@@ -229,3 +255,25 @@ def test_rx_chunk_tails(m, o, torch_cuda, c3_stream):
     iqs.append(host(i_)); ss.append(host(s_))
     assert np.array_equal(np.concatenate(iqs).view(np.uint32), host(iq1).view(np.uint32))
     assert np.array_equal(np.concatenate(ss), host(s1))
+
+
+def test_tx_f16_output_only_4_byte_aligned(m, o, torch_cuda):
+    """An f16 TX output that is only 4-byte aligned (a row-sliced (n, 2) float16 tensor): the
+    whole-line pair stores need 8-byte alignment, so such a call takes the one-sample stores;
+    the samples equal, bit for bit, those of a call into an aligned buffer."""
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS["c3_qam16"]
+    nsym = 300_001
+    bits = torch.from_numpy(o.prng_bits(SEED + 11, nsym * bps)).cuda()
+    taps = m.rrc_taps(L, sps, 0.35)
+    w = o.sample_freq(1, 4)
+
+    def tx():
+        return m.DigitalModulator(m.Carrier(w), product_phasor(m, name), sps, taps, dtype=1)
+    ref = tx().process(bits)
+    big = torch.zeros((ref.shape[0] + 1, 2), dtype=torch.float16, device="cuda")
+    out = big[1:]
+    assert out.data_ptr() % 8 == 4
+    got = tx().process(bits, out=out)
+    assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    assert torch.equal(big[0], torch.zeros(2, dtype=torch.float16, device="cuda"))

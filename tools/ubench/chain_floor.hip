@@ -1,119 +1,124 @@
-// The C3 chain's byte pattern with no compute (the measured practical floor).
-// Per 2^24-sample period: bits in 16 MiB (1 B/sample), samples written 128 MiB, the same samples
-// re-read 128 MiB, decimated I/Q 32 MiB + decisions 4 MiB written (19.25 B/sample, 323 MB).
+// The chains' byte patterns with no compute: the measured practical floor of each bench config
+// (VERDICT r03 item 1 for C3; r04 "missing" item 2 for the out-of-cache configs). Per period:
+// bits in (bps / sps B per sample), samples written (S B) and re-read, decimated I/Q (S / sps)
+// + decisions (1 / sps) written, over the product kernels' tiles of 1024 kept instants
+// (TS = 1024 sps samples), 256 threads per tile, 16-B accesses.
 //
-//   two   : the two launches of the product chain, as streaming kernels over 4096-sample tiles
-//           (tile = the TX/RX kernels' tile: 1024 symbols / 1024 instants at sps 4); the RX
-//           pattern walks tiles top-down as rx_mfma does.
-//   fused : ONE persistent launch, each workgroup alternating TX tile t and RX tile t - G (the
-//           tile it wrote one round earlier; G = the grid), the re-read still through global
-//           loads of the sample buffer.
-//   tx / rx alone, and a plain write-then-read of 128 MiB for reference.
+//   c3   16-QAM sps 4, f32, 2^24 samples (19.25 B/sample, 323 MB): the round-4 variants (fused
+//        TX/RX tiles in one persistent launch, lag G or 0, write-through stores) besides the two
+//        launches
+//   c4   8 QPSK channels x 2^22 (one batch launch pair, 2^25 samples, 18.75 B/sample);
+//   c4g4 4 channels per launch pair (2^24 samples)
+//   c5   256-QAM sps 8, f32, 2^26 samples (18.125 B/sample, 1.22 GB)
+//   c5h  the same with f16 samples (9.625 B/sample, 646 MB)
+// Every config: the two launches with default-policy TX stores, with non-temporal TX stores,
+// with the first half non-temporal (the product's C5 f16 policy), TX alone, RX alone; the RX
+// walks its tiles top-down in rounds of the grid, as rx_mfma does.
 //
-// hipcc -O3 --offload-arch=gfx950 chain_floor.hip -o chain_floor && ./chain_floor
+// hipcc -O3 --offload-arch=gfx950 chain_floor.hip -o chain_floor && ./chain_floor [config|all] [pmc]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
-#define NS (1 << 24)                 // samples per period
-#define TS 4096                      // samples per tile
-#define NT (NS / TS)                 // tiles
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
 
-// TX tile: 4096 bits bytes in (16 B per thread), 32 KiB of samples out (8 float4 per thread).
-__device__ __forceinline__ void tx_tile(const uint4* __restrict__ bits, float4* __restrict__ y, int t) {
-    const uint4 b = bits[(size_t)t * 256 + threadIdx.x];
-    const float v = (float)(b.x ^ b.y ^ b.z ^ b.w);
-    float4* o = y + (size_t)t * (TS * 8 / 16);
+// One config's tile shape. TS samples per tile, S bytes per sample, BB bits bytes per tile,
+// IQB I/Q bytes and SYB decision bytes per tile (all multiples of 16 x 256 or of 4 x 256).
+template <int TS_, int S_, int BB_, int SPS_>
+struct Shape {
+    static constexpr int TS = TS_, S = S_, BB = BB_, SPS = SPS_;
+    static constexpr int YV = TS * S / 16 / 256;        // 16-B sample vectors per thread
+    static constexpr int BV = (BB / 16 + 255) / 256;    // 16-B bit vectors per thread (partial)
+    static constexpr int IQV = TS / SPS * S / 16 / 256; // 16-B I/Q vectors per thread
+    static constexpr int SYW = TS / SPS / 4 / 256;      // 4-B decision words per thread
+    static_assert(YV >= 1 && IQV >= 1 && SYW >= 1, "tile shape");
+};
+
+// TX tile t: bits in, samples out (nt: non-temporal stores, as tx_nt_below)
+template <class C>
+__device__ __forceinline__ void tx_tile(const uint4* __restrict__ bits, uint4* __restrict__ y, int64_t t, bool nt) {
+    unsigned v = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j * 256 + threadIdx.x] = make_float4(v, v + j, v, v - j);
-}
-// RX tile: 32 KiB of samples in (8 float4 per thread), 8 KiB of I/Q (2 float4 per thread) and
-// 1 KiB of decisions (4 B per thread) out.
-__device__ __forceinline__ void rx_tile(const float4* __restrict__ y, float4* __restrict__ iq,
-                                        unsigned* __restrict__ sym, int t) {
-    const float4* x = y + (size_t)t * (TS * 8 / 16);
-    float4 a = make_float4(0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float4 v = x[j * 256 + threadIdx.x];
-        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    for (int k = 0; k < C::BV; ++k) {
+        const int i = k * 256 + threadIdx.x;
+        if (i * 16 < C::BB) {
+            const uint4 b = bits[t * (C::BB / 16) + i];
+            v ^= b.x ^ b.y ^ b.z ^ b.w;
+        }
     }
-    float4* o = iq + (size_t)t * 512;
-    o[threadIdx.x] = a;
-    o[256 + threadIdx.x] = make_float4(a.w, a.z, a.y, a.x);
-    sym[(size_t)t * 256 + threadIdx.x] = __float_as_uint(a.x) & 0x0f0f0f0f;
-}
-
-__global__ __launch_bounds__(256) void k_tx(const uint4* bits, float4* y) {
-    for (int t = blockIdx.x; t < NT; t += gridDim.x) tx_tile(bits, y, t);
-}
-__global__ __launch_bounds__(256) void k_rx(const float4* y, float4* iq, unsigned* sym) {
-    // top-down rounds, as rx_mfma walks C3
-    const int G = gridDim.x, R = (NT + G - 1) / G;
-    for (int r = 0; r < R; ++r) {
-        const int t = NT - (r + 1) * G + blockIdx.x;
-        if (t >= 0) rx_tile(y, iq, sym, t);
+    uint4* o = y + t * (C::TS * C::S / 16);
+#pragma unroll
+    for (int j = 0; j < C::YV; ++j) {
+        const u4v w = {v, v + j, v ^ 5u, v - j};
+        if (nt) __builtin_nontemporal_store(w, reinterpret_cast<u4v*>(o + j * 256 + threadIdx.x));
+        else *reinterpret_cast<u4v*>(o + j * 256 + threadIdx.x) = w;
     }
 }
-__global__ __launch_bounds__(256) void k_fused(const uint4* bits, float4* y, float4* iq, unsigned* sym) {
-    const int G = gridDim.x;
-    int t = blockIdx.x;
-    for (; t < NT; t += G) {
-        tx_tile(bits, y, t);
+// RX tile t: samples in, I/Q and decisions out
+template <class C>
+__device__ __forceinline__ void rx_tile(const uint4* __restrict__ y, uint4* __restrict__ iq, unsigned* __restrict__ sym,
+                                        int64_t t) {
+    const uint4* x = y + t * (C::TS * C::S / 16);
+    uint4 a = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < C::YV; ++j) {
+        const uint4 v = x[j * 256 + threadIdx.x];
+        a.x += v.x; a.y ^= v.y; a.z += v.z; a.w ^= v.w;
+    }
+    uint4* o = iq + t * (C::TS / C::SPS * C::S / 16);
+#pragma unroll
+    for (int j = 0; j < C::IQV; ++j) o[j * 256 + threadIdx.x] = make_uint4(a.x + j, a.y, a.z, a.w);
+#pragma unroll
+    for (int j = 0; j < C::SYW; ++j) sym[t * (C::TS / C::SPS / 4) + j * 256 + threadIdx.x] = (a.x ^ a.z) & 0x0f0f0f0f;
+}
+
+// nt_below: tiles < nt_below store non-temporally
+template <class C>
+__global__ __launch_bounds__(256) void k_tx(const uint4* bits, uint4* y, int64_t nt, int64_t nt_below) {
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) tx_tile<C>(bits, y, t, t < nt_below);
+}
+template <class C>
+__global__ __launch_bounds__(256) void k_rx(const uint4* y, uint4* iq, unsigned* sym, int64_t nt) {
+    const int64_t G = gridDim.x, R = (nt + G - 1) / G;      // top-down rounds, as rx_mfma
+    for (int64_t r = 0; r < R; ++r) {
+        const int64_t t = nt - (r + 1) * G + blockIdx.x;
+        if (t >= 0) rx_tile<C>(y, iq, sym, t);
+    }
+}
+// C3 only (round 4): one persistent launch, TX tile t then RX tile t - G (lag G) or t (lag 0)
+template <class C>
+__global__ __launch_bounds__(256) void k_fused(const uint4* bits, uint4* y, uint4* iq, unsigned* sym, int64_t nt) {
+    const int64_t G = gridDim.x;
+    int64_t t = blockIdx.x;
+    for (; t < nt; t += G) {
+        tx_tile<C>(bits, y, t, false);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t - G >= 0) rx_tile(y, iq, sym, t - G);
+        if (t - G >= 0) rx_tile<C>(y, iq, sym, t - G);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t - G < NT) rx_tile(y, iq, sym, t - G);
+    if (t - G < nt) rx_tile<C>(y, iq, sym, t - G);
 }
-// lag 0: RX tile t right after TX tile t in the same workgroup (the tile just written)
-__global__ __launch_bounds__(256) void k_fused0(const uint4* bits, float4* y, float4* iq, unsigned* sym) {
-    for (int t = blockIdx.x; t < NT; t += gridDim.x) {
-        tx_tile(bits, y, t);
+template <class C>
+__global__ __launch_bounds__(256) void k_fused0(const uint4* bits, uint4* y, uint4* iq, unsigned* sym, int64_t nt) {
+    for (int64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+        tx_tile<C>(bits, y, t, false);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        rx_tile(y, iq, sym, t);
+        rx_tile<C>(y, iq, sym, t);
     }
-}
-// the same with the TX tile stored write-through (sc1: the line leaves the XCD's L2)
-typedef unsigned u4v __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256) void k_fused0_sc1(const uint4* bits, float4* y, float4* iq, unsigned* sym) {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(y, 0, 0x7fffffff, 0x00020000);
-    for (int t = blockIdx.x; t < NT; t += gridDim.x) {
-        const uint4 b = bits[(size_t)t * 256 + threadIdx.x];
-        const float v = (float)(b.x ^ b.y ^ b.z ^ b.w);
-        const unsigned base = (unsigned)t * (TS * 8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            __builtin_amdgcn_raw_buffer_store_b128((u4v){__float_as_uint(v), __float_as_uint(v + j), __float_as_uint(v),
-                                                   __float_as_uint(v - j)}, r, base + (j * 256 + threadIdx.x) * 16, 0, 16);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        rx_tile(y, iq, sym, t);
-    }
-}
-__global__ void k_wr(float4* o, size_t n) {
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        o[i] = make_float4(1, 2, 3, 4);
-}
-__global__ void k_rd(const float4* x, float* o, size_t n) {
-    float4 a = make_float4(0, 0, 0, 0);
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const float4 v = x[i]; a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-    }
-    if (a.x == 12345.f) o[0] = a.y + a.z + a.w;
 }
 
-static bool g_quick = false;                     // argv[1] == "pmc": 3 launches each, untimed
+static bool g_quick = false;                     // "pmc": 3 launches each, untimed
 template <typename F> static void run(const char* name, double bytes, F f) {
     if (g_quick) { for (int i = 0; i < 3; ++i) f(); (void)hipDeviceSynchronize(); printf("%s\n", name); return; }
-    for (int i = 0; i < 200; ++i) f();           // settle the clocks
+    for (int i = 0; i < 100; ++i) f();           // settle the clocks
     (void)hipDeviceSynchronize();
     hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
     float best = 1e30f, sum = 0;
-    const int R = 5, K = 200;
+    const int R = 5, K = 100;
     for (int r = 0; r < R; ++r) {
         (void)hipEventRecord(a);
         for (int k = 0; k < K; ++k) f();
@@ -121,40 +126,67 @@ template <typename F> static void run(const char* name, double bytes, F f) {
         float ms; (void)hipEventElapsedTime(&ms, a, b); ms /= K;
         best = ms < best ? ms : best; sum += ms;
     }
-    printf("%-44s min %7.2f us  mean %7.2f us  %6.2f TB/s (min)\n", name, best * 1e3, sum / R * 1e3,
+    printf("%-50s min %8.2f us  mean %8.2f us  %6.2f TB/s (min)\n", name, best * 1e3, sum / R * 1e3,
            bytes / (best * 1e-3) / 1e12);
     fflush(stdout);
 }
 
-int main(int argc, char** argv) {
-    g_quick = argc > 1 && argv[1][0] == 'p';
-    uint4* bits; float4 *y, *iq; unsigned* sym; float* o;
-    (void)hipMalloc(&bits, (size_t)NS); (void)hipMalloc(&y, (size_t)NS * 8);
-    (void)hipMalloc(&iq, (size_t)NS / 4 * 8); (void)hipMalloc(&sym, (size_t)NS / 4); (void)hipMalloc(&o, 64);
-    (void)hipMemset(bits, 1, (size_t)NS);
-    const double btx = NS * 9.0, brx = NS * 8.0 + NS / 4 * 9.0, bch = btx + brx;
-    int dev = 0, ncu = 0; (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    printf("CUs %d; chain bytes per period %.1f MB (19.25 B/sample)\n", ncu, bch / 1e6);
+template <class C>
+static void config(const char* cname, int64_t nsamp, bool c3_extra, int ncu) {
+    const int64_t nt = nsamp / C::TS;
+    const size_t bb = (size_t)nt * C::BB, yb = (size_t)nsamp * C::S, iqb = (size_t)nsamp / C::SPS * C::S,
+                 syb = (size_t)nsamp / C::SPS;
+    uint4 *bits, *y, *iq; unsigned* sym;
+    if (hipMalloc(&bits, bb) || hipMalloc(&y, yb) || hipMalloc(&iq, iqb) || hipMalloc(&sym, syb)) {
+        printf("%s: hipMalloc failed\n", cname);
+        exit(1);
+    }
+    (void)hipMemset(bits, 1, bb);
+    (void)hipMemset(y, 0, yb);
+    const double btx = (double)bb + yb, brx = (double)yb + iqb + syb, bch = btx + brx;
+    printf("\n[%s] %lld samples, %lld tiles of %d; chain bytes per period %.1f MB (%.4g B/sample)\n", cname,
+           (long long)nsamp, (long long)nt, C::TS, bch / 1e6, bch / nsamp);
     for (int per : {2, 4, 8}) {
         const int G = ncu * per;
-        char n[96];
-        snprintf(n, 96, "two launches (tx; rx top-down) grid %d", G);
-        run(n, bch, [&] { hipLaunchKernelGGL(k_tx, G, 256, 0, 0, bits, y);
-                          hipLaunchKernelGGL(k_rx, G, 256, 0, 0, y, iq, sym); });
-        snprintf(n, 96, "fused (tx t, rx t-G) grid %d", G);
-        run(n, bch, [&] { hipLaunchKernelGGL(k_fused, G, 256, 0, 0, bits, y, iq, sym); });
-        snprintf(n, 96, "fused lag 0 (tx t, rx t) grid %d", G);
-        run(n, bch, [&] { hipLaunchKernelGGL(k_fused0, G, 256, 0, 0, bits, y, iq, sym); });
-        snprintf(n, 96, "fused lag 0, tx sc1 stores grid %d", G);
-        run(n, bch, [&] { hipLaunchKernelGGL(k_fused0_sc1, G, 256, 0, 0, bits, y, iq, sym); });
-        snprintf(n, 96, "tx alone grid %d", G);
-        run(n, btx, [&] { hipLaunchKernelGGL(k_tx, G, 256, 0, 0, bits, y); });
-        snprintf(n, 96, "rx alone grid %d", G);
-        run(n, brx, [&] { hipLaunchKernelGGL(k_rx, G, 256, 0, 0, y, iq, sym); });
+        char n[112];
+        auto two = [&](int64_t ntb) {
+            hipLaunchKernelGGL(k_tx<C>, G, 256, 0, 0, bits, y, nt, ntb);
+            hipLaunchKernelGGL(k_rx<C>, G, 256, 0, 0, y, iq, sym, nt);
+        };
+        snprintf(n, sizeof n, "%s two launches grid %d", cname, G);
+        run(n, bch, [&] { two(0); });
+        snprintf(n, sizeof n, "%s two launches, tx nt stores grid %d", cname, G);
+        run(n, bch, [&] { two(nt); });
+        snprintf(n, sizeof n, "%s two launches, tx first half nt grid %d", cname, G);
+        run(n, bch, [&] { two(nt / 2); });
+        if (c3_extra) {
+            snprintf(n, sizeof n, "%s fused (tx t, rx t-G) grid %d", cname, G);
+            run(n, bch, [&] { hipLaunchKernelGGL(k_fused<C>, G, 256, 0, 0, bits, y, iq, sym, nt); });
+            snprintf(n, sizeof n, "%s fused lag 0 (tx t, rx t) grid %d", cname, G);
+            run(n, bch, [&] { hipLaunchKernelGGL(k_fused0<C>, G, 256, 0, 0, bits, y, iq, sym, nt); });
+        }
+        snprintf(n, sizeof n, "%s tx alone grid %d", cname, G);
+        run(n, btx, [&] { hipLaunchKernelGGL(k_tx<C>, G, 256, 0, 0, bits, y, nt, (int64_t)0); });
+        snprintf(n, sizeof n, "%s tx alone, nt stores grid %d", cname, G);
+        run(n, btx, [&] { hipLaunchKernelGGL(k_tx<C>, G, 256, 0, 0, bits, y, nt, nt); });
+        snprintf(n, sizeof n, "%s rx alone grid %d", cname, G);
+        run(n, brx, [&] { hipLaunchKernelGGL(k_rx<C>, G, 256, 0, 0, y, iq, sym, nt); });
     }
-    const size_t n4 = (size_t)NS * 8 / 16;
-    run("write 128 MiB + read 128 MiB (same buffer)", 2.0 * NS * 8, [&] {
-        hipLaunchKernelGGL(k_wr, 2048, 256, 0, 0, y, n4);
-        hipLaunchKernelGGL(k_rd, 2048, 256, 0, 0, y, o, n4); });
+    (void)hipFree(bits); (void)hipFree(y); (void)hipFree(iq); (void)hipFree(sym);
+}
+
+int main(int argc, char** argv) {
+    const char* which = argc > 1 ? argv[1] : "all";
+    g_quick = argc > 2 && argv[2][0] == 'p';
+    int ncu = 0;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+    printf("CUs %d\n", ncu);
+    auto on = [&](const char* c) { return !strcmp(which, "all") || !strcmp(which, c); };
+    // Shape<samples per tile, bytes per sample, bits bytes per tile, sps>
+    if (on("c3")) config<Shape<4096, 8, 4096, 4>>("c3", 1 << 24, true, ncu);
+    if (on("c4")) config<Shape<4096, 8, 2048, 4>>("c4", 1 << 25, false, ncu);
+    if (on("c4g4")) config<Shape<4096, 8, 2048, 4>>("c4g4", 1 << 24, false, ncu);
+    if (on("c5")) config<Shape<8192, 8, 8192, 8>>("c5", 1 << 26, false, ncu);
+    if (on("c5h")) config<Shape<8192, 4, 8192, 8>>("c5h", 1 << 26, false, ncu);
     return 0;
 }
