@@ -262,4 +262,13 @@ __device__ __forceinline__ void mfma_chain_lb(const float2* arow, OffF off, cons
     }
 }
 
+// The fused small call's LDS sample window (RawOut / RxHandoff): element i lives at raw_pos(i).
+// raw_pos swaps 8-B elements inside aligned groups of 4 by bits 5-6 of the index. The RX reads
+// its staging quads there (lane l: elements 4 l + j): unswizzled, lanes l and l + 8 hit the same
+// bank pair of a ds_read_b64 (bank = element mod 32), a 4-way conflict on every read (C2's
+// chain_small: ~100 conflict cycles per workgroup, 102,400 per launch); swizzled, the 32 lanes of
+// each group cover 32 distinct elements mod 32 for any start. The TX's 16 consecutive lanes per
+// ds_write_b64 group write 16 consecutive elements of a 16-aligned run: still distinct mod 16.
+__device__ __forceinline__ int64_t raw_pos(int64_t i) { return i ^ ((i >> 5) & 3); }
+
 }  // namespace mk

@@ -375,6 +375,17 @@ struct RxMfma {
     // (the matched filter then single-buffers its operands to fit 128 VGPRs), else the
     // compiler's choice.
     static constexpr int WPE = SWZ && (LDS_BYTES <= 40960 || KS == 2) ? 4 : 1;
+#ifndef MODEM_RX_LATE
+#define MODEM_RX_LATE 0
+#endif
+#ifndef MODEM_RX_DB
+#define MODEM_RX_DB 0
+#endif
+    // LATE: the last LATE quad slots of a 1024-instant tile are reloaded with the next tile's
+    // samples after the matched filter instead of during the staging, so that their registers are
+    // free while the filter runs (DBF: it then double-buffers its operands at 4 waves per SIMD).
+    static constexpr int LATE = NWF == 4 && KS == 1 && WPE == 4 ? MODEM_RX_LATE : 0;
+    static constexpr bool DBF = WPE < 4 || (NWF == 4 && KS == 1 && MODEM_RX_DB);
     static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
     // plane offset between staging slots (the swizzle repeats every 1024 samples)
     static constexpr int SLOT_POS = SWZ ? 4 * NT : 4 * NT + 16 * (4 * NT / RW);
@@ -477,7 +488,7 @@ struct RxMfma {
     // fir_part: k-steps [s0, s0 + NS_) of 16-row block blk, summed from zero.
     template <int NS_>
     __device__ static void fir_part(const _Float16* pl, const _Float16* tbl, int blk, int s0, f32x4& dre, f32x4& dim) {
-        constexpr bool DB = WPE < 4;
+        constexpr bool DB = DBF;
         const int lane = tid_() & 63;
         const int i = lane & 15, g = lane >> 4;
         const int ae = (16 * blk + i) * RW + 8 * g + 32 * s0;
@@ -538,12 +549,20 @@ struct RxMfma {
     // barrier, after which the planes may be restaged, and the lower wave adds them and stores.
     template <int EM>
     __device__ __forceinline__ static void filter_emit(const RxParams& p, const _Float16* pl, const _Float16* tbl,
-                                                       f32x4* part, int64_t ot0, int kab) {
+                                                       f32x4* part, int64_t ot0, int kab, QT* pre = nullptr,
+                                                       const __amdgpu_buffer_rsrc_t* nxt = nullptr) {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         f32x4 dre, dim;
         if constexpr (KS == 1) {
             if (NWF == NW || wave < NWF) {     // uniform
                 fir(pl, tbl, dre, dim);
+                if (LATE > 0 && pre) {         // the late slots' reloads (see LATE)
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int voff = 4 * tid_() * (int)sizeof(InT) * 2;
+#pragma unroll
+                    for (int u = UQ - LATE; u < UQ; ++u) pre[u] = load_slot(*nxt, voff, u);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 emit<EM>(p, ot0 + wave * 256, dre, dim, kab);
             }
         } else {
@@ -628,7 +647,7 @@ struct RxMfma {
             if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, pos0 + u * SLOT_POS, zr, zi);
             // (not hoisted above the mix: the slot's registers would be copied out first)
             __builtin_amdgcn_sched_barrier(0);
-            pre[u] = load_slot(nxt, voff, u);                  // the next tile's slot u, same registers
+            if (u < UQ - LATE) pre[u] = load_slot(nxt, voff, u);   // the next tile's slot u, same registers
             __builtin_amdgcn_sched_barrier(0);                 // one quad's temporaries at a time
         }
         if constexpr (P1) {                    // the partial slot, one sample per lane: the quad path's
@@ -759,7 +778,7 @@ struct RxMfma {
                     if constexpr (HO) {                // (samples before the chunk: patched below)
                         const int64_t i = q_lo + (tid + (k0 + b) * NT) - ho.base;
                         const bool in = i >= 0 && i < ho.n && q_lo + (tid + (k0 + b) * NT) < p.N;
-                        v[b] = in ? ho.raw[i] : make_float2(0.f, 0.f);
+                        v[b] = in ? ho.raw[raw_pos(i)] : make_float2(0.f, 0.f);
                     } else {
                         v[b] = ld(rx, (uint32_t)(tid + (k0 + b) * NT - ox) * S);
                     }
@@ -892,7 +911,7 @@ struct RxMfma {
             __syncthreads();
             if (!(fi && fast_ok(votes, kpred))) return;
             if (t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
-            filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb);
+            filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb, pre, &nxt);
             if (KS == 1) __syncthreads();      // the planes are restaged next (KS = 2: in filter_emit)
             w.next();
         }
@@ -940,7 +959,7 @@ struct RxMfma {
                     for (int j = 0; j < 4; ++j) {
                         const int eu = e + 4 * NT * u + j;
                         const int64_t i = w.q + eu - ho.base;
-                        x[j] = eu < 4 * NQ && w.q + eu < p.N && i >= 0 && i < ho.n ? ho.raw[i] : make_float2(0.f, 0.f);
+                        x[j] = eu < 4 * NQ && w.q + eu < p.N && i >= 0 && i < ho.n ? ho.raw[raw_pos(i)] : make_float2(0.f, 0.f);
                     }
                     pre[u] = QT{make_float4(x[0].x, x[0].y, x[1].x, x[1].y), make_float4(x[2].x, x[2].y, x[3].x, x[3].y)};
                 }

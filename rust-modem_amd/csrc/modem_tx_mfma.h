@@ -106,7 +106,8 @@ typedef _Float16 th8 __attribute__((ext_vector_type(8)));
 typedef _Float16 th4 __attribute__((ext_vector_type(4)));
 
 // An LDS copy of the samples a workgroup emits (the fused small call, modem_chain.hip: its RX
-// reads them there instead of from HBM): sample j of the call at p[j - base], 0 <= j - base < n.
+// reads them there instead of from HBM): sample j of the call at p[raw_pos(j - base)],
+// 0 <= j - base < n (n a multiple of 4).
 struct RawOut {
     float2* p;
     int64_t base;
@@ -281,7 +282,7 @@ struct TxMfma {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int64_t i = jt + loff + 16 * r - ro.base;
-                if (i >= 0 && i < ro.n) ro.p[i] = make_float2(z[r].x, z[r].y);
+                if (i >= 0 && i < ro.n) ro.p[raw_pos(i)] = make_float2(z[r].x, z[r].y);
             }
         }
         // wave-uniform base in SGPRs + 32-bit lane byte offsets (saddr + voffset stores)
@@ -346,7 +347,7 @@ struct TxMfma {
             }
             if constexpr (RAW) {
                 const int64_t i = jt + off - ro.base;
-                if (i >= 0 && i < ro.n) ro.p[i] = make_float2(z.x, z.y);
+                if (i >= 0 && i < ro.n) ro.p[raw_pos(i)] = make_float2(z.x, z.y);
             }
             if constexpr (STORE) {
                 if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(p.out, jt + off, z.x);

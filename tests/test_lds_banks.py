@@ -141,3 +141,54 @@ def test_swizzled_layout_conflict_free():
     # a bijection within every aligned group of 8 chunks (no LDS beyond the unpadded plane)
     for base in range(0, 4096, 64):
         assert sorted(swz_pos(e) for e in range(base, base + 64)) == list(range(base, base + 64))
+
+
+# ------------------------------------------------------------------------------------------------
+# The fused small call's LDS sample window (chain_small, modem_chain.hip): the TX writes every
+# emitted sample (8-B float2) at raw_pos(i), the RX stages its quads from it (lane l of a wave reads
+# elements q + 4 l + j, j = 0..3, one ds_read_b64 each). ds_read_b64 is serviced as lanes {0-31},
+# {32-63} with bank = dword mod 64, i.e. element mod 32; ds_write_b64 as 4 groups of 16 contiguous
+# lanes with bank = dword mod 32, i.e. element mod 16 (MI355X_MICROARCH.md §LDS).
+
+def raw_pos(i):                # modem_device.h
+    return i ^ ((i >> 5) & 3)
+
+
+def b64_read_extra(elem):
+    tot = 0
+    for g in (range(0, 32), range(32, 64)):
+        banks = {}
+        for lane in g:
+            banks.setdefault(elem(lane) % 32, set()).add(elem(lane))
+        tot += max(len(v) for v in banks.values()) - 1
+    return tot
+
+
+def b64_write_extra(elem):
+    tot = 0
+    for g in (range(0, 16), range(16, 32), range(32, 48), range(48, 64)):
+        banks = {}
+        for lane in g:
+            banks.setdefault(elem(lane) % 16, set()).add(elem(lane))
+        tot += max(len(v) for v in banks.values()) - 1
+    return tot
+
+
+def test_handoff_window_conflict_free():
+    """RX quad reads from the window at every start offset: 3 extra cycles per group and read
+    unswizzled (4-way, the 102,400 cycles per C2 launch the PMC counter measured), none with
+    raw_pos; the TX's stores (lane l: 64 (l >> 4) + (l & 15) + 16 r from a 16-aligned base) stay
+    conflict-free."""
+    for q in range(0, 64):
+        for j in range(4):
+            assert b64_read_extra(lambda l: q + 4 * l + j) == 6          # 2 groups x (4-way - 1)
+            assert b64_read_extra(lambda l: raw_pos(q + 4 * l + j)) == 0
+    for base in range(0, 1024, 16):
+        for r in range(4):
+            assert b64_write_extra(lambda l: raw_pos(base + 64 * (l >> 4) + (l & 15) + 16 * r)) == 0
+    # the general path's one-sample-per-lane reads (consecutive lanes, consecutive elements) from
+    # a 32-aligned start stay conflict-free
+    for q in range(0, 1024, 32):
+        assert b64_read_extra(lambda l: raw_pos(q + l)) == 0
+    # a permutation inside aligned groups of 4: a window of 4 k elements maps onto itself
+    assert sorted(raw_pos(i) for i in range(4 * 300)) == list(range(4 * 300))

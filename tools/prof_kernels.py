@@ -18,10 +18,17 @@ def main():
     ap.add_argument("--only", choices=["tx", "rx", "both", "chain"], default="both",
                     help="chain: the bench's step (ChainPlan: the fused launch where it applies)")
     ap.add_argument("--amplitude", type=float, default=1.0)
+    # multi-channel configs: the bench's batch launches over groups of --group channels (0: the
+    # config's default), as bench.py runs them; --no-batch: one launch per channel
+    ap.add_argument("--group", type=int, default=0)
+    ap.add_argument("--no-batch", action="store_true")
     a = ap.parse_args()
-    r = bench.GpuRunner(bench.WORKLOADS[a.config], 0, 0, amplitude=a.amplitude)
+    wl, _ = bench.rank_workload(a.config, 1)
+    batch = wl[5] > 1 and not a.no_batch
+    group = a.group if a.group > 0 else bench.GROUP_DEFAULT.get(a.config, 0)
+    r = bench.GpuRunner(wl, 0, 0, amplitude=a.amplitude, batch=batch, group=group)
     for _ in range(a.reps):
-        if a.only == "chain":
+        if a.only == "chain" or batch:
             r.step()
             continue
         for c in range(r.nch):
