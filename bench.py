@@ -482,6 +482,8 @@ def run(args, runner_factory, dist=None, rank=0, world=1):
     dom_traffic = traffic.get(dom[3]) if isinstance(traffic, dict) else None
     if dom[3] == "chain" and isinstance(traffic, dict) and traffic.get("chain_form") != fused:
         dom_traffic = None
+    if isinstance(traffic, dict) and traffic.get("channels_per_launch", per_launch) != per_launch:
+        dom_traffic = None          # measured on another launch size (channel group)
     chain_gbs = b_moved / (t_chain * 1e-3) / 1e9
     out = {
         "metric": METRIC,
