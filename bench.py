@@ -140,6 +140,16 @@ class GpuRunner:
                 self._txp.append(m.TxBatchPlan([d["tx"] for d in ch], [d["bits"] for d in ch], [d["y"] for d in ch]))
                 self._rxp.append(m.RxBatchPlan([d["rx"] for d in ch], [d["y"] for d in ch], [d["oiq"] for d in ch],
                                                [d["osym"] for d in ch]))
+            # the step: one prepared C call for every group (modem_chain_batch_*: the handles and
+            # buffers checked once, not per call), and the first group's pair alone for the chain leg
+            self._cbp = self._cbp0 = None
+            if hasattr(m, "ChainBatchPlan") and hasattr(m.load_library(), "modem_chain_batch_run"):
+                def plan(chs):
+                    return m.ChainBatchPlan([d["tx"] for d in chs], [d["rx"] for d in chs], [d["bits"] for d in chs],
+                                            [d["y"] for d in chs], [d["oiq"] for d in chs], [d["osym"] for d in chs],
+                                            group=self.group)
+                self._cbp = plan(self.ch)
+                self._cbp0 = plan(self.ch[:self.group])
         # one prepared C call per channel and step (modem_chain_run = modem_tx_process +
         # modem_rx_process on the fixed device buffers): the TX and RX kernels of the step with
         # the buffers checked once, so that the host stays ahead of small steps (C2)
@@ -158,6 +168,9 @@ class GpuRunner:
 
     def step(self):
         if self.batch:
+            if self._cbp is not None:
+                self._cbp.run()
+                return
             for txp, rxp in zip(self._txp, self._rxp):
                 txp.run()
                 rxp.run()
@@ -241,6 +254,9 @@ class GpuRunner:
 
     def _step_timed(self):
         if self.batch:
+            if self._cbp0 is not None:
+                self._cbp0.run()
+                return
             self._txp[0].run()
             self._rxp[0].run()
         elif self._plans:

@@ -26,6 +26,9 @@
  *   modem_chain_*            modulator.rs:85-100 then  one period of the sample-buffer loop:
  *                            demodulator.rs:44-56      the DigitalModulator's samples of a bit
  *                                                      buffer, then the Demodulator over them
+ *   modem_chain_batch_*      the same, per channel       one period of a bank of independent
+ *                                                      channels (one modulator and one
+ *                                                      demodulator per stream)
  *
  * Conventions
  *   - Every function returns modem_status (0 = OK, negative = error) and never aborts.
@@ -55,8 +58,9 @@ extern "C" {
 /* 2: modem_tx_desc.q_offset; 3: the channel-batch entry points; 4: modem_rx_desc.phase_offset
  * (the descriptor grew 8 bytes: 80 -> 88), modem_pll_lock, MODEM_DTYPE_I16 and
  * MODEM_MIX_REFERENCE_REAL_EXACT; 5: modem_chain_* (no layout change; modem_chain_fused
- * added later, additive). Layouts: INTEGRATION.md. */
-#define MODEM_HIP_ABI_VERSION 5
+ * added later, additive); 6: modem_chain_batch_* (additive, no layout change). Layouts:
+ * INTEGRATION.md. */
+#define MODEM_HIP_ABI_VERSION 6
 
 typedef enum {
     MODEM_OK = 0,
@@ -279,6 +283,24 @@ modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_
  * forces 0. */
 int modem_chain_fused(const modem_chain* c);
 modem_status modem_chain_destroy(modem_chain* c);
+
+/* A prepared step of a channel bank (independent channel streams, BASELINE
+ * config 4): modem_chain_batch_run(c) equals, for every channel i < nch,
+ *   modem_tx_process(txs[i], bits[i], nbits[i], samples[i], caps[i], &n[i], stream);
+ *   modem_rx_process(rxs[i], samples[i], n[i], out_iq[i], out_sym[i], out_caps[i], &k[i], stream);
+ * run as one TX launch and then one RX launch per `group` consecutive channels (1 <= group <= 8;
+ * a group's samples are re-read while they are still in the Infinity Cache). modem_chain_batch_create
+ * checks the buffers (device memory of the handles' one device) and the handles (one matrix-core
+ * configuration for all TX and one for all RX handles, distinct handles, RX in_dtype = TX dtype,
+ * complex mix, interleaved complex TX output) once: INVALID_ARG / UNSUPPORTED otherwise, nothing
+ * created. produced / produced_out (nch entries each, may be NULL) receive n[i] and k[i]. */
+typedef struct modem_chain_batch modem_chain_batch;
+modem_status modem_chain_batch_create(modem_tx* const* txs, modem_rx* const* rxs, size_t nch, size_t group,
+                                      const uint8_t* const* bits, const size_t* nbits, void* const* samples,
+                                      const size_t* caps, void* const* out_iq, uint8_t* const* out_sym,
+                                      const size_t* out_caps, modem_chain_batch** out);
+modem_status modem_chain_batch_run(modem_chain_batch* c, size_t* produced, size_t* produced_out, void* stream);
+modem_status modem_chain_batch_destroy(modem_chain_batch* c);
 
 /* Demodulator::lock_phase (demodulator.rs:32-36): PLL::handle (pll.rs:16-22) over the n
  * complex samples x_iq (host memory; the reference uses n = 64), with the carrier phases of

@@ -165,6 +165,11 @@ def load_library():
         "modem_chain_run": (st, [vp, c.POINTER(sz), c.POINTER(sz), vp]),
         "modem_chain_fused": (c.c_int, [vp]),
         "modem_chain_destroy": (st, [vp]),
+        "modem_chain_batch_create": (st, [c.POINTER(vp), c.POINTER(vp), sz, sz, c.POINTER(vp), c.POINTER(sz),
+                                          c.POINTER(vp), c.POINTER(sz), c.POINTER(vp), c.POINTER(vp),
+                                          c.POINTER(sz), c.POINTER(vp)]),
+        "modem_chain_batch_run": (st, [vp, c.POINTER(sz), c.POINTER(sz), vp]),
+        "modem_chain_batch_destroy": (st, [vp]),
     }
     for name, (res, args) in sig.items():
         try:
@@ -987,6 +992,62 @@ class ChainPlan:
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:
             _lib.modem_chain_destroy(self._h)
+            self._h = None
+
+
+class ChainBatchPlan:
+    """One period of a bank of independent channels as one C call (modem_chain_batch_*): `run()`
+    equals `ChainPlan(tx[i], rx[i], bits[i], samples[i], out_iq[i], out_sym[i]).run()` for every
+    channel i (the DigitalModulator's samples of each channel's bits, modulator.rs:85-100, then
+    that channel's Demodulator over them, demodulator.rs:44-56), run as one TX launch and then one
+    RX launch per `group` consecutive channels, with the handles and buffers checked once here.
+    Every handle's Python-side state advances as those calls would advance it. Raises ModemPanic
+    (UNSUPPORTED) when the handles do not share one matrix-core configuration per side."""
+
+    def __init__(self, txs, rxs, bits, samples, out_iq, out_sym, group: int = 8):
+        self.txs, self.rxs = list(txs), list(rxs)
+        self.bits, self.samples, self.out_iq, self.out_sym = list(bits), list(samples), list(out_iq), list(out_sym)
+        n = self.n = len(self.txs)
+        if not (len(self.rxs) == len(self.bits) == len(self.samples) == len(self.out_iq) == len(self.out_sym) == n):
+            raise ValueError("ChainBatchPlan: one modulator, demodulator and buffer set per channel")
+        for tx, rx, y, oiq, osym in zip(self.txs, self.rxs, self.samples, self.out_iq, self.out_sym):
+            if tx.dtype != rx.in_dtype or tx.out_mode == OUT_REAL:
+                raise ValueError("ChainBatchPlan: each RX must read its TX's interleaved samples (one dtype)")
+            _check_rx_input(y, tx.dtype, "ChainBatchPlan samples")
+            want_out = _IN_DTYPE_NAME[rx.out_dtype]
+            if len(oiq.shape) != 2 or int(oiq.shape[1]) != 2 or _dtype_name(oiq) != want_out:
+                raise ValueError(f"ChainBatchPlan: out_iq must be (k, 2) {want_out}, got {tuple(oiq.shape)} {_dtype_name(oiq)}")
+            if len(osym.shape) != 1 or _dtype_name(osym) != "uint8":
+                raise ValueError(f"ChainBatchPlan: out_sym must be (k,) uint8, got {tuple(osym.shape)} {_dtype_name(osym)}")
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        self._nb = [int(b.numel() if _is_torch(b) else b.size) for b in self.bits]
+        txh = (vp * n)(*[t._h.value for t in self.txs])
+        rxh = (vp * n)(*[r._h.value for r in self.rxs])
+        outc = (sz * n)(*[min(int(a.shape[0]), int(b.shape[0])) for a, b in zip(self.out_iq, self.out_sym)])
+        h = ctypes.c_void_p()
+        _check(load_library().modem_chain_batch_create(
+            txh, rxh, n, int(group), (vp * n)(*[_ptr(b) for b in self.bits]), (sz * n)(*self._nb),
+            (vp * n)(*[_ptr(y) for y in self.samples]), (sz * n)(*[int(y.shape[0]) for y in self.samples]),
+            (vp * n)(*[_ptr(x) for x in self.out_iq]), (vp * n)(*[_ptr(x) for x in self.out_sym]), outc,
+            ctypes.byref(h)), "ChainBatchPlan")
+        self._h = h
+        self._prod, self._kout = (sz * n)(), (sz * n)()
+        self._fn = load_library().modem_chain_batch_run
+
+    def run(self, stream=None):
+        """Returns (samples produced, kept instants produced) per channel."""
+        _check(self._fn(self._h, self._prod, self._kout, _stream_handle(stream, self.txs[0].device)),
+               "ChainBatchPlan.run")
+        for tx, rx, k, n in zip(self.txs, self.rxs, self._nb, self._prod):
+            tx._ncarry = (tx._ncarry + k) % tx.bps
+            tx.carrier.sample += n
+            rx._consumed += n
+            rx.carrier.sample += n
+        return list(self._prod), list(self._kout)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.modem_chain_batch_destroy(self._h)
             self._h = None
 
 

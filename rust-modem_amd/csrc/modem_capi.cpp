@@ -1188,6 +1188,133 @@ int modem_chain_fused(const modem_chain* c) { return c ? c->last : -1; }
 
 modem_status modem_chain_destroy(modem_chain* c) { delete c; return MODEM_OK; }
 
+// ----------------------------------------------------------------------- chain batch ----
+// A prepared period of a channel bank over fixed device buffers (BASELINE config 4): the
+// handles' batch compatibility and the buffers' kinds are checked once here (modem_tx_process_batch
+// and modem_rx_process_batch check them on every call: a pointer-attribute query per buffer and a
+// comparison of the handles' fragment tables, ~10 us per 4-channel TX call, which held C4's
+// channel groups to the host's rate), so a run is the launches and the state updates.
+struct modem_chain_batch {
+    std::vector<modem_tx*> tx;
+    std::vector<modem_rx*> rx;
+    std::vector<const uint8_t*> bits;
+    std::vector<size_t> nbits, caps, out_caps;
+    std::vector<void*> samples, out_iq;
+    std::vector<uint8_t*> out_sym;
+    size_t group = mk::kBatchMax;
+};
+
+modem_status modem_chain_batch_create(modem_tx* const* txs, modem_rx* const* rxs, size_t nch, size_t group,
+                                      const uint8_t* const* bits, const size_t* nbits, void* const* samples,
+                                      const size_t* caps, void* const* out_iq, uint8_t* const* out_sym,
+                                      const size_t* out_caps, modem_chain_batch** out) {
+    if (!out) return MODEM_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (!txs || !rxs || nch == 0 || group < 1 || group > (size_t)mk::kBatchMax || !bits || !nbits || !samples ||
+        !caps || !out_iq || !out_sym || !out_caps)
+        return MODEM_ERR_INVALID_ARG;
+    const modem_tx* t0 = txs[0];
+    const modem_rx* r0 = rxs[0];
+    if (!t0 || !r0) return MODEM_ERR_INVALID_ARG;
+    const int dev = t0->device;
+    for (size_t c = 0; c < nch; ++c) {
+        const modem_tx* t = txs[c];
+        const modem_rx* r = rxs[c];
+        if (!t || !r || t->device != dev || r->device != dev || !samples[c] || (nbits[c] && !bits[c]))
+            return MODEM_ERR_INVALID_ARG;
+        for (size_t e = 0; e < c; ++e)
+            if (txs[e] == t || rxs[e] == r) return MODEM_ERR_INVALID_ARG;   // a handle at most once
+        // the RX reads what the TX writes: interleaved complex samples of one dtype
+        if (t->out_mode != MODEM_OUT_IQ_MIXED || r->in_dtype != t->dtype) return MODEM_ERR_INVALID_ARG;
+        if ((nbits[c] && ptr_kind(bits[c], dev) != PTR_DEVICE) || ptr_kind(samples[c], dev) != PTR_DEVICE ||
+            (out_iq[c] && ptr_kind(out_iq[c], dev) != PTR_DEVICE) ||
+            (out_sym[c] && ptr_kind(out_sym[c], dev) != PTR_DEVICE))
+            return MODEM_ERR_INVALID_ARG;
+        // one matrix-core configuration per side (the batch kernels' conditions)
+        if (t->ph_kind != 0 || t->mfma_ksteps <= 0 || t->mfma_ksteps != t0->mfma_ksteps || t->dtype != t0->dtype ||
+            t->sps != t0->sps || t->bps != t0->bps || t->ntaps != t0->ntaps || t->q_offset != 0 ||
+            t->bfrag_host != t0->bfrag_host)
+            return MODEM_ERR_UNSUPPORTED;
+        if (r->mfma_ksteps <= 0 || r->mfma_ksteps != r0->mfma_ksteps || r->mix != MODEM_MIX_COMPLEX ||
+            r->in_dtype != r0->in_dtype || r->out_dtype != r->in_dtype || r->decim != r0->decim ||
+            r->ntaps != r0->ntaps || r->bfrag_host != r0->bfrag_host)
+            return MODEM_ERR_UNSUPPORTED;
+    }
+    modem_chain_batch* b = new (std::nothrow) modem_chain_batch;
+    if (!b) return MODEM_ERR_ALLOC;
+    b->tx.assign(txs, txs + nch);
+    b->rx.assign(rxs, rxs + nch);
+    b->bits.assign(bits, bits + nch);
+    b->nbits.assign(nbits, nbits + nch);
+    b->samples.assign(samples, samples + nch);
+    b->caps.assign(caps, caps + nch);
+    b->out_iq.assign(out_iq, out_iq + nch);
+    b->out_sym.assign(out_sym, out_sym + nch);
+    b->out_caps.assign(out_caps, out_caps + nch);
+    b->group = group;
+    *out = b;
+    return MODEM_OK;
+}
+
+modem_status modem_chain_batch_run(modem_chain_batch* b, size_t* produced, size_t* produced_out, void* stream) {
+    if (!b) return MODEM_ERR_INVALID_ARG;
+    const size_t nch = b->tx.size();
+    const hipStream_t s = (hipStream_t)stream;
+    // every channel's call sizes first: an error leaves every handle untouched
+    int64_t nsym[mk::kBatchMax], k_first[mk::kBatchMax], nout[mk::kBatchMax];
+    int ncarry_new[mk::kBatchMax];
+    for (size_t c = 0; c < nch; ++c) {
+        const modem_tx* t = b->tx[c];
+        const uint64_t total = (uint64_t)t->ncarry + b->nbits[c];
+        const int64_t ns = (int64_t)(total / t->bps);
+        if ((size_t)ns * t->sps > b->caps[c]) return MODEM_ERR_CAPACITY;
+        int64_t k0, k;
+        rx_range(b->rx[c]->consumed, b->rx[c]->consumed + ns * (int64_t)t->sps, b->rx[c]->decim, b->rx[c]->D, &k0, &k);
+        if ((size_t)k > b->out_caps[c]) return MODEM_ERR_CAPACITY;
+    }
+    DeviceGuard g(b->tx[0]->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    for (size_t c0 = 0; c0 < nch; c0 += b->group) {
+        const int n = (int)std::min(b->group, nch - c0);
+        mk::TxBatch tb{};
+        tb.nch = n;
+        uint64_t launch_bytes = 0;
+        for (int i = 0; i < n; ++i) {
+            const size_t c = c0 + (size_t)i;
+            const modem_tx* t = b->tx[c];
+            const uint64_t total = (uint64_t)t->ncarry + b->nbits[c];
+            nsym[i] = (int64_t)(total / t->bps);
+            ncarry_new[i] = (int)(total - (uint64_t)nsym[i] * t->bps);
+            const size_t ns = (size_t)nsym[i] * t->sps;
+            tx_fill(t, b->bits[c], b->nbits[c], false, b->samples[c], nsym[i], ncarry_new[i], ns, tb.p[i]);
+            launch_bytes += (uint64_t)ns * tx_sample_bytes(t);
+        }
+        for (int i = 0; i < n; ++i)
+            tb.p[i].nt_below = tx_nt_below(nsym[i] * (int64_t)b->tx[c0 + i]->sps, launch_bytes, false);
+        const modem_tx* t0 = b->tx[c0];
+        HIP_TRY(mk::launch_tx_mfma_batch(tb, (int)t0->sps, t0->mfma_ksteps, t0->d_bfrag, t0->dtype, s));
+        mk::RxBatch rb{};
+        rb.nch = n;
+        for (int i = 0; i < n; ++i) {
+            const size_t c = c0 + (size_t)i;
+            modem_tx* t = b->tx[c];
+            const size_t ns = (size_t)nsym[i] * t->sps;
+            tx_advance(t, false, nsym[i], ncarry_new[i], ns);
+            modem_rx* r = b->rx[c];
+            rx_range(r->consumed, r->consumed + (int64_t)ns, r->decim, r->D, &k_first[i], &nout[i]);
+            rx_fill(r, b->samples[c], ns, b->out_iq[c], b->out_sym[c], k_first[i], nout[i], rb.p[i]);
+            if (produced) produced[c] = ns;
+            if (produced_out) produced_out[c] = (size_t)nout[i];
+        }
+        const modem_rx* r0 = b->rx[c0];
+        HIP_TRY(mk::launch_rx_mfma_batch(rb, (int)r0->decim, r0->mfma_ksteps, r0->d_bfrag, r0->in_dtype, s));
+        for (int i = 0; i < n; ++i) rx_advance(b->rx[c0 + i], (size_t)nsym[i] * b->tx[c0 + i]->sps);
+    }
+    return MODEM_OK;
+}
+
+modem_status modem_chain_batch_destroy(modem_chain_batch* b) { delete b; return MODEM_OK; }
+
 // ----------------------------------------------------------------------------- FIR ----
 struct modem_fir {
     int device = 0;

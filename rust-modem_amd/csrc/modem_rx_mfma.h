@@ -381,6 +381,9 @@ struct RxMfma {
 #ifndef MODEM_RX_DB
 #define MODEM_RX_DB 0
 #endif
+#ifndef MODEM_RX_HI_NOLO       // experiment: f16 in and out, the taps' f16 roundings only
+#define MODEM_RX_HI_NOLO 0
+#endif
     // LATE: the last LATE quad slots of a 1024-instant tile are reloaded with the next tile's
     // samples after the matched filter instead of during the staging, so that their registers are
     // free while the filter runs (DBF: it then double-buffers its operands at 4 waves per SIMD).
@@ -518,8 +521,10 @@ struct RxMfma {
             else if (s + 1 < NS_) load(s + 1, c ^ 1);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][0], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
-            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
-            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][1], m0, 0, 0, 0);
+            if (!(HI && MODEM_RX_HI_NOLO)) {
+                r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
+                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][1], m0, 0, 0, 0);
+            }
             if (!HI) {
                 r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], b[c][0], r0, 0, 0, 0);
                 m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], b[c][0], m0, 0, 0, 0);

@@ -86,13 +86,16 @@ __device__ __forceinline__ uint32_t word_index(uint64_t v, int bps) {
 // same k positions and a stream cut into calls gives the same samples as one call.
 // Sample-and-hold (no taps) stays on the exact VALU kernels.
 #ifndef MODEM_TX_WIDE
-#define MODEM_TX_WIDE 0
+#define MODEM_TX_WIDE 1
 #endif
 template <int SPS, int SUB_> struct TxMfmaCfg {
     static constexpr int SB = 16 / SPS;          // symbols per row-block
     static constexpr int NT = 256;               // 4 waves
-    // 16x16 tiles per wave per tile: 4, 1 (small calls); WIDE: 8 at sps 8 (1024-symbol tiles,
-    // the 94-symbol window halo 8 % of the staged symbols instead of 16 %)
+    // 16x16 tiles per wave per tile: 4, 1 (small calls); at sps 8, 8 (round 5, MODEM_TX_WIDE):
+    // 1024-symbol tiles like sps 4's, so the 94-symbol window halo is 8 % of the staged symbols
+    // instead of 16 %, and a TX tile is exactly one RX tile (8192 samples), written on the XCD that
+    // reads it back. C5 chain 259 -> 245.6 us (the RX in the chain 154.3 -> 142.8), C5 f16 175.2 ->
+    // 169.2 us (profiles/r05_tx_wide.txt).
     static constexpr int SUB = SUB_ == 4 && SPS == 8 && MODEM_TX_WIDE ? 8 : SUB_;
     static constexpr int TS = 4 * SUB * 16 * SB; // symbols per workgroup tile
     static constexpr int NCOP = SB % 4 == 0 ? 1 : 4 / SB;   // plane copies (8-B aligned A reads)

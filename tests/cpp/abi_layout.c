@@ -17,7 +17,7 @@
 #define _Alignof alignof
 #endif
 
-static_assert(MODEM_HIP_ABI_VERSION == 5, "the layouts below are ABI version 5 (unchanged since 4)");
+static_assert(MODEM_HIP_ABI_VERSION == 6, "the layouts below are ABI version 6 (unchanged since 4)");
 
 SZ(modem_ring, 12, 4)
 OF(modem_ring, start, 0) OF(modem_ring, end, 1) OF(modem_ring, radius, 4) OF(modem_ring, phase, 8)
