@@ -150,6 +150,16 @@ class GpuRunner:
                                             group=self.group)
                 self._cbp = plan(self.ch)
                 self._cbp0 = plan(self.ch[:self.group])
+            # experiment switch (A/B only): MODEM_BENCH_BATCH=plans runs the per-group TX / RX
+            # batch plans instead; =streams2 one prepared call per group, group k on HIP stream
+            # k % 2 (a group's RX beside the next group's TX)
+            self._mode = os.environ.get("MODEM_BENCH_BATCH", "")
+            if self._mode == "plans":
+                self._cbp = None
+            elif self._mode == "streams2" and self._cbp is not None:
+                self._gplans = [plan(self.ch[c0:c0 + self.group]) for c0 in range(0, nch, self.group)]
+                if len(self.streams) < 2:
+                    self.streams.append(torch.cuda.Stream())
         # one prepared C call per channel and step (modem_chain_run = modem_tx_process +
         # modem_rx_process on the fixed device buffers): the TX and RX kernels of the step with
         # the buffers checked once, so that the host stays ahead of small steps (C2)
@@ -168,6 +178,13 @@ class GpuRunner:
 
     def step(self):
         if self.batch:
+            if self._mode == "streams2" and self._cbp is not None:
+                s0, s1 = self.streams[0], self.streams[1]
+                s1.wait_stream(s0)
+                for k, pl in enumerate(self._gplans):
+                    pl.run(stream=s0 if k % 2 == 0 else s1)
+                s0.wait_stream(s1)
+                return
             if self._cbp is not None:
                 self._cbp.run()
                 return

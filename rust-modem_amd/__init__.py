@@ -1001,8 +1001,8 @@ class ChainBatchPlan:
     channel i (the DigitalModulator's samples of each channel's bits, modulator.rs:85-100, then
     that channel's Demodulator over them, demodulator.rs:44-56), run as one TX launch and then one
     RX launch per `group` consecutive channels, with the handles and buffers checked once here.
-    Every handle's Python-side state advances as those calls would advance it. Raises ModemPanic
-    (UNSUPPORTED) when the handles do not share one matrix-core configuration per side."""
+    Every handle's Python-side state advances as those calls would advance it. Raises ModemError
+    (MODEM_ERR_UNSUPPORTED) when the handles do not share one matrix-core configuration per side."""
 
     def __init__(self, txs, rxs, bits, samples, out_iq, out_sym, group: int = 8):
         self.txs, self.rxs = list(txs), list(rxs)

@@ -14,16 +14,16 @@ pytestmark = pytest.mark.gpu
 
 
 def bank(m, torch, name, nch, nsamp, seed0, dtype=0):
-    _, bps, L, sps = CONFIGS[name]
+    ph_name, bps, L, sps = CONFIGS[name]
     taps = m.rrc_taps(L, sps, 0.35)
     w = m.Freq(1, 4).sample_freq()
     tdt = torch.float16 if dtype else torch.float32
     out = []
     for c in range(nch):
-        ph = product_phasor(m, name)
+        ph = product_phasor(m, ph_name)
         tx = m.DigitalModulator(m.Carrier(w), ph, sps, taps, dtype=dtype)
         rx = m.DemodulatorRx(m.Carrier(w), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
-                             slicer=product_phasor(m, name).slicer(), in_dtype=dtype, out_dtype=dtype)
+                             slicer=product_phasor(m, ph_name).slicer(), in_dtype=dtype, out_dtype=dtype)
         bits = m.prng_bits(seed0 + c, nsamp // sps * bps)
         y = torch.empty((nsamp, 2), dtype=tdt, device="cuda")
         oiq = torch.empty((nsamp // sps, 2), dtype=tdt, device="cuda")
@@ -68,8 +68,9 @@ def test_batch_plan_refusals(m, torch_cuda):
     c3 = bank(m, torch, "c3_qam16", 1, 1 << 16, 9)
     cols = lambda ds: ([d["tx"] for d in ds], [d["rx"] for d in ds], [d["bits"] for d in ds], [d["y"] for d in ds],
                        [d["oiq"] for d in ds], [d["osym"] for d in ds])
-    with pytest.raises(m.ModemPanic):                   # two filter configurations in one bank
+    with pytest.raises(m.ModemError) as e:              # two filter configurations in one bank
         m.ChainBatchPlan(*cols(a + c3))
+    assert e.value.status == -2                         # MODEM_ERR_UNSUPPORTED
     with pytest.raises(m.ModemPanic):                   # a handle twice
         m.ChainBatchPlan(*cols([a[0], a[0]]))
     with pytest.raises(m.ModemPanic):                   # group outside 1..8
