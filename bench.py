@@ -54,7 +54,7 @@ WORKLOADS = {
 FIXED_TOTAL = {"c4"}
 # channels per TX / RX launch pair of a multi-channel step (the batch entry points take up to 8
 # per launch, modem_internal.h kBatchMax); the groups run one after another, TX then RX each
-GROUP_DEFAULT = {"c4": 8}
+GROUP_DEFAULT = {"c4": 4}
 
 
 def rank_workload(config, world):
@@ -151,22 +151,41 @@ class GpuRunner:
                 self._cbp = plan(self.ch)
                 self._cbp0 = plan(self.ch[:self.group])
             # experiment switch (A/B only): MODEM_BENCH_BATCH=plans runs the per-group TX / RX
-            # batch plans instead; =streams2 one prepared call per group, group k on HIP stream
-            # k % 2 (a group's RX beside the next group's TX)
-            self._mode = os.environ.get("MODEM_BENCH_BATCH", "")
-            if self._mode == "plans":
+            # batch plans instead of the prepared call
+            if os.environ.get("MODEM_BENCH_BATCH", "") == "plans":
                 self._cbp = None
-            elif self._mode == "streams2" and self._cbp is not None:
-                self._gplans = [plan(self.ch[c0:c0 + self.group]) for c0 in range(0, nch, self.group)]
-                if len(self.streams) < 2:
-                    self.streams.append(torch.cuda.Stream())
         # one prepared C call per channel and step (modem_chain_run = modem_tx_process +
         # modem_rx_process on the fixed device buffers): the TX and RX kernels of the step with
         # the buffers checked once, so that the host stays ahead of small steps (C2)
         chain = hasattr(m.load_library(), "modem_chain_run")   # (experiment builds of older sources: no)
         self._plans = None if batch or not chain else [
             m.ChainPlan(d["tx"], d["rx"], d["bits"], d["y"], d["oiq"], d["osym"]) for d in self.ch]
+        # experiment (A/B only): MODEM_BENCH_PIPE=1 pipelines consecutive periods of a one-channel
+        # config: period k's TX writes sample buffer k % 2 on one stream while period k - 1's RX
+        # reads the other buffer on a second stream (events order TX k -> RX k, RX k - 2 -> TX k)
+        self._pipe = os.environ.get("MODEM_BENCH_PIPE", "") == "1" and not batch and nch == 1
+        if self._pipe:
+            d = self.ch[0]
+            self._ys = [d["y"], torch.empty_like(d["y"])]
+            self._sb = torch.cuda.Stream()
+            self._ev_tx = [torch.cuda.Event(), torch.cuda.Event()]
+            self._ev_rx = [None, None]
+            self._k = 0
         torch.cuda.synchronize()
+
+    def _pipe_step(self):
+        d, k = self.ch[0], self._k
+        y, sa, sb = self._ys[k % 2], self.stream, self._sb
+        if self._ev_rx[k % 2] is not None:
+            sa.wait_event(self._ev_rx[k % 2])          # RX k - 2 has read this buffer
+        d["tx"].process(d["bits"], out=y, stream=sa)
+        self._ev_tx[k % 2].record(sa)
+        sb.wait_event(self._ev_tx[k % 2])
+        d["rx"].process(y, out_iq=d["oiq"], out_sym=d["osym"], stream=sb)
+        ev = self._ev_rx[k % 2] or torch.cuda.Event()
+        ev.record(sb)
+        self._ev_rx[k % 2] = ev
+        self._k += 1
 
     def tx(self, c, stream=None):
         d = self.ch[c]
@@ -177,14 +196,9 @@ class GpuRunner:
         d["rx"].process(d["y"], out_iq=d["oiq"], out_sym=d["osym"], stream=stream)
 
     def step(self):
+        if self._pipe:
+            return self._pipe_step()
         if self.batch:
-            if self._mode == "streams2" and self._cbp is not None:
-                s0, s1 = self.streams[0], self.streams[1]
-                s1.wait_stream(s0)
-                for k, pl in enumerate(self._gplans):
-                    pl.run(stream=s0 if k % 2 == 0 else s1)
-                s0.wait_stream(s1)
-                return
             if self._cbp is not None:
                 self._cbp.run()
                 return

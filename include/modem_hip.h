@@ -293,7 +293,11 @@ modem_status modem_chain_destroy(modem_chain* c);
  * checks the buffers (device memory of the handles' one device) and the handles (one matrix-core
  * configuration for all TX and one for all RX handles, distinct handles, RX in_dtype = TX dtype,
  * complex mix, interleaved complex TX output) once: INVALID_ARG / UNSUPPORTED otherwise, nothing
- * created. produced / produced_out (nch entries each, may be NULL) receive n[i] and k[i]. */
+ * created. produced / produced_out (nch entries each, may be NULL) receive n[i] and k[i].
+ * With more than one group the groups alternate between `stream` and a stream of the plan's
+ * own (joined to `stream` by events at the start and end of every run), so that one group's RX
+ * overlaps the next group's TX; the run is asynchronous on `stream` as a whole.
+ * MODEM_CHAIN_BATCH_LANES=1 in the environment at create time keeps every launch on `stream`. */
 typedef struct modem_chain_batch modem_chain_batch;
 modem_status modem_chain_batch_create(modem_tx* const* txs, modem_rx* const* rxs, size_t nch, size_t group,
                                       const uint8_t* const* bits, const size_t* nbits, void* const* samples,
