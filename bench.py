@@ -54,7 +54,7 @@ WORKLOADS = {
 FIXED_TOTAL = {"c4"}
 # channels per TX / RX launch pair of a multi-channel step (the batch entry points take up to 8
 # per launch, modem_internal.h kBatchMax); the groups run one after another, TX then RX each
-GROUP_DEFAULT = {"c4": 4}
+GROUP_DEFAULT = {"c4": 8}
 
 
 def rank_workload(config, world):
@@ -182,7 +182,7 @@ class GpuRunner:
         self._ev_tx[k % 2].record(sa)
         sb.wait_event(self._ev_tx[k % 2])
         d["rx"].process(y, out_iq=d["oiq"], out_sym=d["osym"], stream=sb)
-        ev = self._ev_rx[k % 2] or torch.cuda.Event()
+        ev = self._ev_rx[k % 2] or self.torch.cuda.Event()
         ev.record(sb)
         self._ev_rx[k % 2] = ev
         self._k += 1

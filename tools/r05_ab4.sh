@@ -9,8 +9,8 @@ line() { python3 -c "
 import json;d=json.loads([l for l in open('$1') if l.startswith('{')][-1]);c=d['chain_roofline']
 print('$2', d['value'], d['ms_per_step'], 'chain', c['chain_ms'], d['decisions_match_sent'])"; }
 for rep in 1 2; do
-  for g in 4 8; do
-    for lanes in 2 1; do
+  for g in 8; do
+    for lanes in 2; do
       MODEM_CHAIN_BATCH_LANES=$lanes timeout -k 10 300 python3 bench.py --config c4 --group $g $B > $o/c4_g${g}_l$lanes.json 2> $o/err || { tail -3 $o/err; exit 1; }
       line $o/c4_g${g}_l$lanes.json "c4 g$g lanes$lanes"
     done
