@@ -160,32 +160,7 @@ class GpuRunner:
         chain = hasattr(m.load_library(), "modem_chain_run")   # (experiment builds of older sources: no)
         self._plans = None if batch or not chain else [
             m.ChainPlan(d["tx"], d["rx"], d["bits"], d["y"], d["oiq"], d["osym"]) for d in self.ch]
-        # experiment (A/B only): MODEM_BENCH_PIPE=1 pipelines consecutive periods of a one-channel
-        # config: period k's TX writes sample buffer k % 2 on one stream while period k - 1's RX
-        # reads the other buffer on a second stream (events order TX k -> RX k, RX k - 2 -> TX k)
-        self._pipe = os.environ.get("MODEM_BENCH_PIPE", "") == "1" and not batch and nch == 1
-        if self._pipe:
-            d = self.ch[0]
-            self._ys = [d["y"], torch.empty_like(d["y"])]
-            self._sb = torch.cuda.Stream()
-            self._ev_tx = [torch.cuda.Event(), torch.cuda.Event()]
-            self._ev_rx = [None, None]
-            self._k = 0
         torch.cuda.synchronize()
-
-    def _pipe_step(self):
-        d, k = self.ch[0], self._k
-        y, sa, sb = self._ys[k % 2], self.stream, self._sb
-        if self._ev_rx[k % 2] is not None:
-            sa.wait_event(self._ev_rx[k % 2])          # RX k - 2 has read this buffer
-        d["tx"].process(d["bits"], out=y, stream=sa)
-        self._ev_tx[k % 2].record(sa)
-        sb.wait_event(self._ev_tx[k % 2])
-        d["rx"].process(y, out_iq=d["oiq"], out_sym=d["osym"], stream=sb)
-        ev = self._ev_rx[k % 2] or self.torch.cuda.Event()
-        ev.record(sb)
-        self._ev_rx[k % 2] = ev
-        self._k += 1
 
     def tx(self, c, stream=None):
         d = self.ch[c]
@@ -196,8 +171,6 @@ class GpuRunner:
         d["rx"].process(d["y"], out_iq=d["oiq"], out_sym=d["osym"], stream=stream)
 
     def step(self):
-        if self._pipe:
-            return self._pipe_step()
         if self.batch:
             if self._cbp is not None:
                 self._cbp.run()
