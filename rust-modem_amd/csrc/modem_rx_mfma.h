@@ -890,9 +890,6 @@ struct RxMfma {
                 const int64_t n = (sq.first - tmin) / -sq.step + 1;
                 w.nfull = (int32_t)(n < sq.count ? n : sq.count);
             }
-#ifdef MODEM_RX_NOGEN          // timing experiment only: every tile on the fast path (wrong results)
-            w.nfull = w.count;
-#endif
         }
         return w;
     }
