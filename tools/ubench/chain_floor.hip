@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void k_fused(const uint4* bits, uint4* y, uint
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t - G < nt) rx_tile<C>(y, iq, sym, t - G);
+    if (t - G >= 0 && t - G < nt) rx_tile<C>(y, iq, sym, t - G);   // (a grid larger than the tiles: none)
 }
 template <class C>
 __global__ __launch_bounds__(256) void k_fused0(const uint4* bits, uint4* y, uint4* iq, unsigned* sym, int64_t nt) {
