@@ -1094,20 +1094,6 @@ modem_status modem_rx_destroy(modem_rx* h) { delete h; return MODEM_OK; }
 // queries and staging decisions, ~1 us of host time each per call).
 struct modem_chain {
     bool fused = true;
-    // MODEM_CHAIN_SPLIT=k (k >= 2) at create: a period's two launches run as k chunks on two lanes
-    // (chunk i's TX on the caller's stream, its RX on the plan's own stream after it), so that chunk
-    // i's RX overlaps chunk i + 1's TX (experiment; results equal one call's, chunked calls being
-    // bit-identical to one call).
-    int split = 1;
-    hipStream_t side = nullptr;
-    hipEvent_t ev_start = nullptr, ev_end = nullptr;
-    std::vector<hipEvent_t> ev_tx;
-    ~modem_chain() {
-        for (hipEvent_t e : ev_tx) (void)hipEventDestroy(e);
-        if (ev_start) (void)hipEventDestroy(ev_start);
-        if (ev_end) (void)hipEventDestroy(ev_end);
-        if (side) (void)hipStreamDestroy(side);
-    }
     int last = -1;             // how the last run ran (modem_chain_fused)
     bool verbose = false;      // MODEM_CHAIN_VERBOSE=1: why a run took the two launches (stderr)
     modem_tx* tx = nullptr;
@@ -1140,18 +1126,6 @@ modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits,
     c->fused = !(env && env[0] == '0');
     const char* verb = std::getenv("MODEM_CHAIN_VERBOSE");
     c->verbose = verb && verb[0] == '1';
-    const char* sp = std::getenv("MODEM_CHAIN_SPLIT");
-    const int k = sp ? std::atoi(sp) : 1;
-    if (k >= 2 && k <= 16) {
-        DeviceGuard g(dev);
-        c->ev_tx.assign((size_t)k, nullptr);
-        bool ok = g.ok && hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess &&
-                  hipEventCreateWithFlags(&c->ev_start, hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&c->ev_end, hipEventDisableTiming) == hipSuccess;
-        for (int i = 0; ok && i < k; ++i) ok = hipEventCreateWithFlags(&c->ev_tx[i], hipEventDisableTiming) == hipSuccess;
-        if (!ok) { (void)hipGetLastError(); delete c; return MODEM_ERR_HIP; }
-        c->split = k;
-    }
     *out = c;
     return MODEM_OK;
 }
@@ -1199,37 +1173,6 @@ modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_
         }
         if (e != hipErrorNotSupported) { (void)hipGetLastError(); return MODEM_ERR_HIP; }
         if (c->verbose) std::fprintf(stderr, "modem_chain_run: no fused form for this call (two launches)\n");
-    }
-    if (c->split > 1 && tx->ncarry == 0 && c->nbits % tx->bps == 0 && nsym >= (int64_t)c->split * 4096) {
-        // k chunks of whole 1024-symbol tiles on two lanes: TX i on `s`, RX i on the side lane after it
-        const int k = c->split;
-        const int64_t per = nsym / k / 1024 * 1024;
-        HIP_TRY(hipEventRecord(c->ev_start, s));
-        HIP_TRY(hipStreamWaitEvent(c->side, c->ev_start, 0));
-        int64_t sym0 = 0;
-        size_t kout = 0;
-        for (int i = 0; i < k; ++i) {
-            const int64_t ns = i == k - 1 ? nsym - sym0 : per;
-            const size_t n = (size_t)ns * tx->sps;
-            void* smp = static_cast<char*>(c->samples) + (size_t)sym0 * tx->sps * tx_sample_bytes(tx);
-            if ((st = tx_launch(tx, c->bits + (size_t)sym0 * tx->bps, (size_t)ns * tx->bps, false, smp, ns, 0, n, s)))
-                return st;
-            HIP_TRY(hipEventRecord(c->ev_tx[i], s));
-            HIP_TRY(hipStreamWaitEvent(c->side, c->ev_tx[i], 0));
-            int64_t k0, kn;
-            rx_range(rx->consumed, rx->consumed + (int64_t)n, rx->decim, rx->D, &k0, &kn);
-            void* oiq = kn && c->out_iq ? static_cast<char*>(c->out_iq) + kout * rx_out_bytes(rx) : nullptr;
-            uint8_t* osym = kn && c->out_sym ? c->out_sym + kout : nullptr;
-            if ((st = rx_launch(rx, smp, n, oiq, osym, k0, kn, c->side))) return st;
-            kout += (size_t)kn;
-            sym0 += ns;
-        }
-        HIP_TRY(hipEventRecord(c->ev_end, c->side));
-        HIP_TRY(hipStreamWaitEvent(s, c->ev_end, 0));
-        c->last = 0;
-        *produced = nsamp;
-        *produced_out = kout;
-        return MODEM_OK;
     }
     if ((st = tx_launch(tx, c->bits, c->nbits, false, c->samples, nsym, ncarry_new, nsamp, s))) return st;
     if ((st = rx_launch(rx, c->samples, nsamp, nout ? c->out_iq : nullptr, nout ? c->out_sym : nullptr, k_first,
