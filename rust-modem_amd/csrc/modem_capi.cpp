@@ -1094,21 +1094,6 @@ modem_status modem_rx_destroy(modem_rx* h) { delete h; return MODEM_OK; }
 // queries and staging decisions, ~1 us of host time each per call).
 struct modem_chain {
     bool fused = true;
-    // Experiment (MODEM_CHAIN_PIPE=1 at create; timing only, not an ABI contract): odd periods
-    // write their samples to a buffer of the plan's own, and each period's RX runs on the plan's
-    // own stream, so period k's RX overlaps period k + 1's TX; the caller's stream is joined to
-    // period k - 1's RX at the end of run k (the bench synchronises the device).
-    bool pipe = false;
-    long long period = 0;
-    Stage alt;
-    hipStream_t side = nullptr;
-    hipEvent_t ev_tx = nullptr, ev_rx[2] = {nullptr, nullptr};
-    bool rx_rec[2] = {false, false};
-    ~modem_chain() {
-        if (ev_tx) (void)hipEventDestroy(ev_tx);
-        for (hipEvent_t e : ev_rx) if (e) (void)hipEventDestroy(e);
-        if (side) (void)hipStreamDestroy(side);
-    }
     int last = -1;             // how the last run ran (modem_chain_fused)
     bool verbose = false;      // MODEM_CHAIN_VERBOSE=1: why a run took the two launches (stderr)
     modem_tx* tx = nullptr;
@@ -1141,17 +1126,6 @@ modem_status modem_chain_create(modem_tx* tx, modem_rx* rx, const uint8_t* bits,
     c->fused = !(env && env[0] == '0');
     const char* verb = std::getenv("MODEM_CHAIN_VERBOSE");
     c->verbose = verb && verb[0] == '1';
-    const char* pp = std::getenv("MODEM_CHAIN_PIPE");
-    if (pp && pp[0] == '1') {
-        DeviceGuard g(dev);
-        const bool ok = g.ok && c->alt.ensure(cap * tx_sample_bytes(tx)) == MODEM_OK &&
-                        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) == hipSuccess &&
-                        hipEventCreateWithFlags(&c->ev_tx, hipEventDisableTiming) == hipSuccess &&
-                        hipEventCreateWithFlags(&c->ev_rx[0], hipEventDisableTiming) == hipSuccess &&
-                        hipEventCreateWithFlags(&c->ev_rx[1], hipEventDisableTiming) == hipSuccess;
-        if (!ok) { (void)hipGetLastError(); delete c; return MODEM_ERR_HIP; }
-        c->pipe = true;
-    }
     *out = c;
     return MODEM_OK;
 }
@@ -1199,25 +1173,6 @@ modem_status modem_chain_run(modem_chain* c, size_t* produced, size_t* produced_
         }
         if (e != hipErrorNotSupported) { (void)hipGetLastError(); return MODEM_ERR_HIP; }
         if (c->verbose) std::fprintf(stderr, "modem_chain_run: no fused form for this call (two launches)\n");
-    }
-    if (c->pipe) {
-        const int b = (int)(c->period & 1);
-        void* y = b ? c->alt.p : c->samples;
-        if (c->rx_rec[b]) HIP_TRY(hipStreamWaitEvent(s, c->ev_rx[b], 0));      // RX k - 2 has read y
-        if ((st = tx_launch(tx, c->bits, c->nbits, false, y, nsym, ncarry_new, nsamp, s))) return st;
-        HIP_TRY(hipEventRecord(c->ev_tx, s));
-        HIP_TRY(hipStreamWaitEvent(c->side, c->ev_tx, 0));
-        if ((st = rx_launch(rx, y, nsamp, nout ? c->out_iq : nullptr, nout ? c->out_sym : nullptr, k_first, nout,
-                            c->side)))
-            return st;
-        HIP_TRY(hipEventRecord(c->ev_rx[b], c->side));
-        c->rx_rec[b] = true;
-        if (c->rx_rec[b ^ 1]) HIP_TRY(hipStreamWaitEvent(s, c->ev_rx[b ^ 1], 0));   // join period k - 1
-        ++c->period;
-        c->last = 0;
-        *produced = nsamp;
-        *produced_out = (size_t)nout;
-        return MODEM_OK;
     }
     if ((st = tx_launch(tx, c->bits, c->nbits, false, c->samples, nsym, ncarry_new, nsamp, s))) return st;
     if ((st = rx_launch(rx, c->samples, nsamp, nout ? c->out_iq : nullptr, nout ? c->out_sym : nullptr, k_first,
