@@ -416,7 +416,7 @@ template <int SPS, int NKS, int OM, typename OutT, int SUB>
 static hipError_t txm_go_sub(const TxParams& p, const void* bfrag, hipStream_t s) {
     using K = TxMfma<SPS, NKS, OM, OutT, SUB>;
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
-    const size_t lds = MODEM_TX_DBUF && SUB == 4 ? (size_t)K::DB_HALVES * 2 : (size_t)K::PLANES * 2 + ((size_t)1 << p.bps) * 8;
+    const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << p.bps) * 8;
     const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT, SUB>);
     hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT, SUB>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
                        dim3(K::NT), lds, s, p, static_cast<const th8*>(bfrag));
@@ -435,7 +435,7 @@ static hipError_t txm_go_batch_sub(TxBatch b, const void* bfrag, hipStream_t s) 
         const int64_t t = (b.p[c].nsym + b.p[c].lead + K::TS - 1) / K::TS;
         ntiles = t > ntiles ? t : ntiles;
     }
-    const size_t lds = MODEM_TX_DBUF && SUB == 4 ? (size_t)K::DB_HALVES * 2 : (size_t)K::PLANES * 2 + ((size_t)1 << b.p[0].bps) * 8;
+    const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << b.p[0].bps) * 8;
     const void* k = reinterpret_cast<const void*>(&tx_mfma_batch<SPS, NKS, OM, OutT, SUB>);
     const int64_t cap = persistent_grid(k, K::NT, lds, INT64_MAX);
     int64_t g = cap / b.nch;

@@ -141,11 +141,6 @@ struct TxMfma {
     static constexpr int CRES = SB == 2 ? 28 : SB == 1 ? 16 : 0;
     static constexpr int CST = 4 * PLN + (NCOP > 1 ? (CRES - (4 * PLN) % 64 + 64) % 64 : 0);
     static constexpr int PLANES = NCOP * CST;
-    // DBUF (experiment, MODEM_TX_DBUF): a second plane set after the LUT (at most 256 entries of
-    // 4 halves), so that the next full tile is staged while this one's filter runs: one barrier
-    // per tile instead of two. Halves of LDS the standalone TX kernels then need:
-    static constexpr int DB_OFF = PLANES + 1024;
-    static constexpr int DB_HALVES = DB_OFF + PLANES;
     // f16 samples out (the f16 storage sweep, tolerance 2^-10): the taps' f16 roundings only (the
     // lo B fragments carry bits below the f16 output's precision: +2^-12.2 of max|y| before the
     // output rounding on C5, tests/test_gpu_range.py), 2 MFMAs per rail and k-step instead of 3
@@ -476,10 +471,9 @@ struct TxMfma {
 
     // Tiles t0, t0 + ts, ... below t1 (xs > 0: first the last xs sub-tiles of tile t0 - 1). Tile t holds symbols [t*TS - lead, (t+1)*TS - lead) of the call. BPS > 0: bits aligned,
     // no leftover bits, carrier index < 2^53 (the steady state); BPS == 0: general path only.
-    template <int BPS, bool DBUF = false>
+    template <int BPS>
     __device__ __forceinline__ static void run(const TxParams& p, _Float16* pl, th4* lut_s, const th8 (&bh)[NKS],
-                               const th8 (&bl)[NKS], int64_t t0, int64_t t1, int64_t ts, int xs = 0,
-                               _Float16* pl2 = nullptr) {
+                               const th8 (&bl)[NKS], int64_t t0, int64_t t1, int64_t ts, int xs = 0) {
         const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
         const int lead = p.lead;
         const int kab = p.lut_scale_exp + p.tap_scale_exp;
@@ -512,41 +506,7 @@ struct TxMfma {
         __syncthreads();   // LUT visible
         if (xs > 0 && t0 > 0) tail(p, pl, lut_s, bh, bl, t0 - 1, xs, unscale);
         while (t < t1) {
-            if (DBUF && full(t)) {
-                if (!ready) prefetch(t);
-                ready = false;
-                _Float16* cur = pl;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int e = tid + NT * u;
-                    if (e < NE) put(cur, e, lut_s[word_index(pre[u], BPS)]);
-                }
-                __syncthreads();
-                for (; t < t1 && full(t); t += ts) {
-                    const bool more = t + ts < t1 && full(t + ts);
-                    if (t + ts < t1) prefetch(t + ts);   // next bits fly during the MFMAs
-                    const int64_t j0 = (t * TS - lead) * SPS;
-#pragma unroll
-                    for (int q = 0; q < SUB; ++q) {
-                        f32x4 dre, dim;
-                        if (lv) fir<true>(cur, q, bh, bl, dre, dim);
-                        else fir<false>(cur, q, bh, bl, dre, dim);
-                        __builtin_amdgcn_s_setprio(1);
-                        emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
-                        __builtin_amdgcn_s_setprio(0);
-                    }
-                    _Float16* other = cur == pl ? pl2 : pl;
-                    if (more) {                          // the next tile into the other plane set
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            const int e = tid + NT * u;
-                            if (e < NE) put(other, e, lut_s[word_index(pre[u], BPS)]);
-                        }
-                    }
-                    __syncthreads();                     // staged, and every read of `cur` done
-                    cur = other;
-                }
-            } else if (full(t)) {
+            if (full(t)) {
                 if (!ready) prefetch(t);
                 ready = false;
                 for (; t < t1 && full(t); t += ts) {
@@ -611,17 +571,12 @@ __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __res
     // (measured 1 % faster on C3 than contiguous ranges per workgroup)
     const int64_t t0 = bid, t1 = ntiles, ts = nb;
     if (t0 >= t1) return;
-#ifndef MODEM_TX_DBUF
-#define MODEM_TX_DBUF 0
-#endif
-    constexpr bool DB = MODEM_TX_DBUF && SUB == 4;                // the launchers size the LDS for it
-    _Float16* pl2 = lds_t + K::DB_OFF;
     if (p.fast_bits && p.exact_idx) {              // one uniform switch: the tile loop is specialised
         switch (p.bps) {
-        case 1: K::template run<1, DB>(p, pl, lut_s, bh, bl, t0, t1, ts, 0, pl2); return;
-        case 2: K::template run<2, DB>(p, pl, lut_s, bh, bl, t0, t1, ts, 0, pl2); return;
-        case 4: K::template run<4, DB>(p, pl, lut_s, bh, bl, t0, t1, ts, 0, pl2); return;
-        case 8: K::template run<8, DB>(p, pl, lut_s, bh, bl, t0, t1, ts, 0, pl2); return;
+        case 1: K::template run<1>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 2: K::template run<2>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 4: K::template run<4>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
+        case 8: K::template run<8>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
         }
     }
     K::template run<0>(p, pl, lut_s, bh, bl, t0, t1, ts);
