@@ -8,8 +8,9 @@ I/Q + u8 decisions. Workload per GPU is BASELINE config 3 (16-QAM, 129-tap RRC, 
 16 M samples); with --gpus N each rank runs its own independent channel (weak scaling, no
 data-path collective — SURVEY.md §8e). `--config c4` is BASELINE config 4 as the one job it
 names: 64 QPSK channels of 2^22 samples over the node, 64 / N per GPU (strong scaling), each
-step running the rank's channels in groups of 8 (a TX launch, then an RX launch, per group).
-`value` = samples processed by all ranks / the max over ranks of the timed region. Before the warmup each rank runs --settle-ms (300) of untimed
+step running the rank's channels in groups of 8 (a TX launch, then an RX launch, per group;
+consecutive groups alternate between two HIP streams: modem_chain_batch_*).
+`value` = samples processed by all ranks / the max over ranks of the timed region. Before the warmup each rank runs --settle-ms (500) of untimed
 back-to-back steps: the device clock dips for the first ~100 ms of sustained load, and the
 driver's 20-step region (~1.2 ms) would otherwise measure that transient (tools/region_probe.py).
 
@@ -640,7 +641,7 @@ def _parser():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=2000)
     ap.add_argument("--config", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--settle-ms", type=float, default=300.0)
+    ap.add_argument("--settle-ms", type=float, default=500.0)
     ap.add_argument("--cpu-samples", type=int, default=1 << 25)   # ~15 s of oracle work
     ap.add_argument("--no-cpu-baseline", action="store_true")
     # HIP streams the channels of a multi-channel config are spread over (0: one per channel,

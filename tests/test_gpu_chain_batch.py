@@ -78,3 +78,25 @@ def test_batch_plan_refusals(m, torch_cuda):
     t, r, bits, y, oiq, osym = cols(a)
     with pytest.raises(m.ModemPanic):                   # host memory
         m.ChainBatchPlan(t, r, [bits[0], bits[1].cpu().numpy()], y, oiq, osym)
+
+
+def test_batch_plan_one_lane_equals_two_lanes(m, torch_cuda, monkeypatch):
+    """MODEM_CHAIN_BATCH_LANES=1 (every launch on the caller's stream) and the default two lanes
+    (groups alternating between the caller's stream and the plan's own) give the same samples,
+    I/Q and decisions, bit for bit, and both finish on the caller's stream (no explicit sync of
+    the plan's stream: torch's stream-ordered reads see the results)."""
+    torch = torch_cuda
+    outs = []
+    for lanes in ("1", "2"):
+        monkeypatch.setenv("MODEM_CHAIN_BATCH_LANES", lanes)
+        a = bank(m, torch, "c4_qpsk", 6, 1 << 18, 0x5EED3000)
+        plan = m.ChainBatchPlan([d["tx"] for d in a], [d["rx"] for d in a], [d["bits"] for d in a],
+                                [d["y"] for d in a], [d["oiq"] for d in a], [d["osym"] for d in a], group=2)
+        for _ in range(2):
+            plan.run()
+        s = torch.cuda.current_stream()
+        outs.append([torch.cat([d["y"].view(torch.int32).flatten(), d["oiq"].view(torch.int32).flatten(),
+                                d["osym"].to(torch.int32)]).clone() for d in a])
+        s.synchronize()
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
