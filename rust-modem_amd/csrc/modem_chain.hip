@@ -50,13 +50,8 @@ void chain_mfma(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
     {
         _Float16* pl = lds_c;
         th4* lut_s = reinterpret_cast<th4*>(lds_c + TK::PLANES);
-        const int lane = threadIdx.x & 63;
         th8 bh[NKS_T], bl[NKS_T];
-#pragma unroll
-        for (int s = 0; s < NKS_T; ++s) {
-            bh[s] = bfrag[(2 * s) * 64 + lane];
-            bl[s] = bfrag[(2 * s + 1) * 64 + lane];
-        }
+        load_bfrag(bfrag, bh, bl);
         bool done = false;
         if (tp.fast_bits && tp.exact_idx) {
             done = true;
@@ -127,13 +122,8 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
         _Float16* pl = lds_s;
         _Float16* pl2 = lds_s + TK::PLANES;
         th4* lut_s = reinterpret_cast<th4*>(lds_s + 2 * TK::PLANES);
-        const int lane = threadIdx.x & 63;
         th8 bh[NKS_T], bl[NKS_T];
-#pragma unroll
-        for (int s = 0; s < NKS_T; ++s) {
-            bh[s] = bfrag[(2 * s) * 64 + lane];
-            bl[s] = bfrag[(2 * s + 1) * 64 + lane];
-        }
+        load_bfrag(bfrag, bh, bl);
         bool done = false;
         if (tp.fast_bits && tp.exact_idx) {
             done = true;

@@ -113,46 +113,70 @@ __device__ __forceinline__ cf2 cmac(cf2 x, float h, cf2 acc) {
 }
 
 
+// Output buffers are device (global) memory: every sample store goes through an address-space-1
+// view of the caller's pointer, so that it compiles to global_store (counted in vmcnt only). A
+// store through a generic pointer is a flat_store, which also counts in lgkmcnt: the compiler then
+// cannot wait for an LDS read alone while one is in flight, and every LDS wait after a sample store
+// became `s_waitcnt vmcnt(0) lgkmcnt(0)` -- the TX filter's first MFMA of each 16x16 sub-tile waited
+// for all the wave's earlier sample stores to complete (profiles/r05_tx_global_stores.txt).
+template <typename T> using gptr = __attribute__((address_space(1))) T*;
+template <typename T> __device__ __forceinline__ gptr<T> gcast(void* p) { return (gptr<T>)p; }
+typedef float gv2f __attribute__((ext_vector_type(2)));     // (HIP's float2 / float4 classes cannot be
+typedef float gv4f __attribute__((ext_vector_type(4)));     // assigned through an address-space-1 pointer)
+typedef uint32_t gv2u __attribute__((ext_vector_type(2)));
+
+// Buffer descriptor over `bytes` bytes at `base` (wave-uniform inputs made provably uniform).
+// Accesses past `bytes` load zeros / are dropped without touching memory.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// Cache policy of a buffer store (its aux immediate on gfx950): 0 default, 2 non-temporal.
+enum { BUF_DEFAULT = 0, BUF_NT = 2 };
+
 template <typename OutT> struct OutIO;
 template <> struct OutIO<float> {
     __device__ static void store_pair(void* out, int64_t j, float a, float b, float c, float d) {
-        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + 2 * j) = make_float4(a, b, c, d);
+        *gcast<gv4f>(reinterpret_cast<float*>(out) + 2 * j) = (gv4f){a, b, c, d};
     }
     __device__ static void store_one(void* out, int64_t j, float a, float b) {
-        *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + 2 * j) = make_float2(a, b);
+        *gcast<gv2f>(reinterpret_cast<float*>(out) + 2 * j) = (gv2f){a, b};
     }
     __device__ static void store_one_nt(void* out, int64_t j, float a, float b) {   // non-temporal
-        typedef float v2f __attribute__((ext_vector_type(2)));
-        __builtin_nontemporal_store((v2f){a, b}, reinterpret_cast<v2f*>(reinterpret_cast<float*>(out) + 2 * j));
+        __builtin_nontemporal_store((gv2f){a, b}, gcast<gv2f>(reinterpret_cast<float*>(out) + 2 * j));
     }
     __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
-        *reinterpret_cast<float2*>(reinterpret_cast<float*>(out) + j) = make_float2(a, b);
+        *gcast<gv2f>(reinterpret_cast<float*>(out) + j) = (gv2f){a, b};
     }
     __device__ static void store_real_one(void* out, int64_t j, float a) {
-        reinterpret_cast<float*>(out)[j] = a;
+        *gcast<float>(reinterpret_cast<float*>(out) + j) = a;
     }
 };
 template <> struct OutIO<__half> {
     __device__ static void store_pair(void* out, int64_t j, float a, float b, float c, float d) {
         const __half2 h0 = __floats2half2_rn(a, b), h1 = __floats2half2_rn(c, d);
-        uint2 u;
-        u.x = *reinterpret_cast<const uint32_t*>(&h0);
-        u.y = *reinterpret_cast<const uint32_t*>(&h1);
-        *reinterpret_cast<uint2*>(reinterpret_cast<__half*>(out) + 2 * j) = u;
+        *gcast<gv2u>(reinterpret_cast<__half*>(out) + 2 * j) =
+            (gv2u){*reinterpret_cast<const uint32_t*>(&h0), *reinterpret_cast<const uint32_t*>(&h1)};
     }
     __device__ static void store_one(void* out, int64_t j, float a, float b) {
-        *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + 2 * j) = __floats2half2_rn(a, b);
+        const __half2 h = __floats2half2_rn(a, b);
+        *gcast<uint32_t>(reinterpret_cast<__half*>(out) + 2 * j) = *reinterpret_cast<const uint32_t*>(&h);
     }
     __device__ static void store_one_nt(void* out, int64_t j, float a, float b) {   // non-temporal
         const __half2 h = __floats2half2_rn(a, b);
         __builtin_nontemporal_store(*reinterpret_cast<const uint32_t*>(&h),
-                                    reinterpret_cast<uint32_t*>(reinterpret_cast<__half*>(out) + 2 * j));
+                                    gcast<uint32_t>(reinterpret_cast<__half*>(out) + 2 * j));
     }
     __device__ static void store_real_pair(void* out, int64_t j, float a, float b) {
-        *reinterpret_cast<__half2*>(reinterpret_cast<__half*>(out) + j) = __floats2half2_rn(a, b);
+        const __half2 h = __floats2half2_rn(a, b);
+        *gcast<uint32_t>(reinterpret_cast<__half*>(out) + j) = *reinterpret_cast<const uint32_t*>(&h);
     }
     __device__ static void store_real_one(void* out, int64_t j, float a) {
-        reinterpret_cast<__half*>(out)[j] = __float2half_rn(a);
+        const __half h = __float2half_rn(a);
+        *gcast<uint16_t>(reinterpret_cast<__half*>(out) + j) = *reinterpret_cast<const uint16_t*>(&h);
     }
 };
 

@@ -269,15 +269,6 @@ struct RxHandoff {
     int kin;
 };
 
-// Buffer descriptor over `bytes` bytes at `base` (wave-uniform inputs made provably uniform).
-// Accesses past `bytes` load zeros / are dropped without touching memory.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
-    const uint64_t a = reinterpret_cast<uint64_t>(base);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
-                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
 // clamp(v, 0, cap) of a wave-uniform 64-bit value with 32-bit scalar ops on its halves (a
 // 64-bit compare would go through the vector unit: v_cmp_*_i64 from SGPR pairs).
 __device__ __forceinline__ uint32_t clamp64_u32(int64_t v, uint32_t cap) {

@@ -190,15 +190,22 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
     }
 }
 
+// Experiment switch (A/B builds only): MODEM_TX_WPE=4 asks for 4 waves per SIMD (<= 128 VGPRs)
+#ifdef MODEM_TX_WPE
+#define TX_WPE __attribute__((amdgpu_waves_per_eu(MODEM_TX_WPE)))
+#else
+#define TX_WPE
+#endif
+
 template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
-__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
+__global__ __launch_bounds__(256) TX_WPE void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
     tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, blockIdx.x, gridDim.x);
 }
 
 // A batch of independent channels of one configuration (modem_tx_process_batch): workgroup
 // b serves channel b / g as its workgroup b % g of g.
 template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
-__global__ __launch_bounds__(256) void tx_mfma_batch(const TxBatch b, const th8* __restrict__ bfrag) {
+__global__ __launch_bounds__(256) TX_WPE void tx_mfma_batch(const TxBatch b, const th8* __restrict__ bfrag) {
     const int ch = (int)(blockIdx.x / (unsigned)b.g);
     const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
     const TxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg

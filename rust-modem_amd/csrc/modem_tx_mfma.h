@@ -293,44 +293,54 @@ struct TxMfma {
                 if (i >= 0 && i < ro.n) ro.p[raw_pos(i)] = make_float2(z[r].x, z[r].y);
             }
         }
-        // wave-uniform base in SGPRs + 32-bit lane byte offsets (saddr + voffset stores)
+        // The sub-tile's 256 samples through a buffer descriptor at its wave-uniform first sample
+        // (lane byte offsets < 256 samples): buffer stores count in vmcnt only (a store through a
+        // generic pointer is a flat_store, also counted in lgkmcnt, and made every later LDS wait a
+        // wait for all the wave's sample stores), and the non-temporal policy is an immediate of
+        // the store, so the two forms below stay two instructions (as plain global stores under a
+        // uniform branch, the compiler merged them and dropped the non-temporal hint).
         constexpr int SBYTES = (OUT_MODE == OUT_REAL ? 1 : 2) * (int)sizeof(OutT);
-        const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
-        char* ob = reinterpret_cast<char*>(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(oa >> 32)) << 32) |
-                                           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)oa));
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(reinterpret_cast<const char*>(p.out) + jt * SBYTES, 256 * SBYTES);
+        const bool nt = jt < p.nt_below;                    // uniform: past the Infinity Cache (tx_nt_below)
         // f16 samples (4 B): a lane's one-sample stores would leave every 16-lane group
         // writing half a 128-B line. Neighbour lanes swap one packed sample (DPP) so that the
         // even lane holds samples i, i+1 of row r and the odd one samples i-1, i of row r+1:
         // each 8-B store instruction then writes rows r and r+1 of the group, one whole line.
-        // Every such store lands at oa + 8 k, so the form needs oa 8-byte aligned (uniform); a
-        // caller's f16 buffer that is only 4-byte aligned (a sliced (n, 2) tensor) or a
-        // sub-tile at an odd call sample takes the one-sample stores below.
+        // Every such store lands at out + 8 k, so the form needs an 8-byte aligned first sample
+        // (uniform); a caller's f16 buffer that is only 4-byte aligned (a sliced (n, 2) tensor)
+        // or a sub-tile at an odd call sample takes the one-sample stores below.
+        const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
         if (std::is_same<OutT, __half>::value && OUT_MODE != OUT_REAL && (oa & 7) == 0) {
-            typedef uint32_t u2v __attribute__((ext_vector_type(2)));
             const bool odd = lane & 1;
 #pragma unroll
             for (int r = 0; r < 4; r += 2) {
                 const uint32_t a = __builtin_bit_cast(uint32_t, __floats2half2_rn(z[r].x, z[r].y));
                 const uint32_t b = __builtin_bit_cast(uint32_t, __floats2half2_rn(z[r + 1].x, z[r + 1].y));
                 const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? a : b), 0xB1, 0xF, 0xF, false);
-                const uint2 v = odd ? make_uint2(recv, b) : make_uint2(a, recv);
-                char* q = ob + (uint32_t)((odd ? loff + 16 * (r + 1) - 1 : loff + 16 * r) * SBYTES);
-                if (jt < p.nt_below) {          // uniform: past the Infinity Cache (tx_nt_below)
-                    __builtin_nontemporal_store((u2v){v.x, v.y}, reinterpret_cast<u2v*>(q));
-                } else {
-                    *reinterpret_cast<uint2*>(q) = v;
-                }
+                const gv2u v = odd ? (gv2u){recv, b} : (gv2u){a, recv};
+                const int vo = (odd ? loff + 16 * (r + 1) - 1 : loff + 16 * r) * SBYTES;
+                if (nt) __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_NT);
+                else __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_DEFAULT);
             }
-        } else if (OUT_MODE != OUT_REAL && jt < p.nt_below) {     // uniform: past the Infinity Cache (tx_nt_below)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                OutIO<OutT>::store_one_nt(ob + (uint32_t)((loff + 16 * r) * SBYTES), 0, z[r].x, z[r].y);
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                char* q = ob + (uint32_t)((loff + 16 * r) * SBYTES);
-                if (OUT_MODE == OUT_REAL) OutIO<OutT>::store_real_one(q, 0, z[r].x);
-                else OutIO<OutT>::store_one(q, 0, z[r].x, z[r].y);
+                const int vo = (loff + 16 * r) * SBYTES;
+                if constexpr (OUT_MODE == OUT_REAL) {
+                    if constexpr (std::is_same<OutT, float>::value)
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z[r].x), rs, vo, 0, BUF_DEFAULT);
+                    else
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, __float2half_rn(z[r].x)), rs, vo, 0,
+                                                              BUF_DEFAULT);
+                } else if constexpr (std::is_same<OutT, float>::value) {
+                    const gv2u v = __builtin_bit_cast(gv2u, z[r]);
+                    if (nt) __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_NT);
+                    else __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_DEFAULT);
+                } else {
+                    const uint32_t v = __builtin_bit_cast(uint32_t, __floats2half2_rn(z[r].x, z[r].y));
+                    if (nt) __builtin_amdgcn_raw_buffer_store_b32(v, rs, vo, 0, BUF_NT);
+                    else __builtin_amdgcn_raw_buffer_store_b32(v, rs, vo, 0, BUF_DEFAULT);
+                }
             }
         }
     }
@@ -550,6 +560,30 @@ struct TxMfma {
     }
 };
 
+// This lane's B fragments (hi, lo) per k-step, from the host-built table. Each is pinned in its
+// registers right here (an opaque asm use: the loads are waited for once, at the kernel's start):
+// left pending, the compiler's wait tracking merged them into the tile loop's head and made the
+// first MFMA of every tile wait for the next tile's bits prefetch (s_waitcnt vmcnt(3) of 5).
+template <int NKS>
+__device__ __forceinline__ void load_bfrag(const th8* __restrict__ bfrag, th8 (&bh)[NKS], th8 (&bl)[NKS]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        bh[s] = bfrag[(2 * s) * 64 + lane];
+        bl[s] = bfrag[(2 * s + 1) * 64 + lane];
+    }
+#ifndef MODEM_TX_PIN_B          // experiment switch (A/B builds only)
+#define MODEM_TX_PIN_B 1
+#endif
+#if MODEM_TX_PIN_B
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+        asm volatile("" : "+v"(bh[s]));
+        asm volatile("" : "+v"(bl[s]));
+    }
+#endif
+}
+
 // One channel's share of a launch: workgroup `bid` of `nb` working on channel p.
 template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
 __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __restrict__ bfrag,
@@ -558,14 +592,9 @@ __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __res
     extern __shared__ __attribute__((aligned(16))) _Float16 lds_t[];
     _Float16* pl = lds_t;
     th4* lut_s = reinterpret_cast<th4*>(lds_t + K::PLANES);
-    const int tid = threadIdx.x, lane = tid & 63;
     if (bid == 0) tx_state_update(p);
     th8 bh[NKS], bl[NKS];                        // this lane's B fragments (hi, lo) per k-step
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-        bh[s] = bfrag[(2 * s) * 64 + lane];
-        bl[s] = bfrag[(2 * s + 1) * 64 + lane];
-    }
+    load_bfrag(bfrag, bh, bl);
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
     // tiles bid, bid + nb, ...: concurrently running workgroups work on neighbouring tiles
     // (measured 1 % faster on C3 than contiguous ranges per workgroup)

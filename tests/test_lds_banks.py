@@ -192,3 +192,32 @@ def test_handoff_window_conflict_free():
         assert b64_read_extra(lambda l: raw_pos(q + l)) == 0
     # a permutation inside aligned groups of 4: a window of 4 k elements maps onto itself
     assert sorted(raw_pos(i) for i in range(4 * 300)) == list(range(4 * 300))
+
+
+def test_tx_lut_gather_conflicts_match_pmc():
+    """The sps-8 TX's LDS bank conflicts are its symbol-LUT gathers, not the plane copies.
+
+    The fast TX staging looks each symbol up in an LDS copy of the split LUT (tx_mfma, 8 B per
+    entry, one ds_read_b64 per lane and staging slot: two groups of 32 lanes, bank = dword mod 64).
+    256-QAM's random indices spread 32 lanes over 32 bank pairs, so a read costs the largest
+    number of distinct entries on one pair, minus one, per group. Over C5's launch (2^23 symbols,
+    8192 tiles of NE = 1024 + 94 window symbols, one lane per symbol) the model gives the
+    SQ_LDS_BANK_CONFLICT both C5 TX launches measured (615,682, profiles/r05_c5h_pmc_summary.txt
+    and r05_c5_pmc_summary.txt), i.e. ~2.4 K LDS cycles per CU in an 83-104 us launch; 16-QAM's
+    16 entries sit on 16 distinct pairs (C3's TX: 0)."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+
+    def extra(nent, trials):
+        tot = 0
+        for _ in range(trials):
+            e = rng.integers(0, nent, 64)
+            for g in (e[:32], e[32:]):
+                u = np.unique(g)
+                tot += np.bincount((2 * u) % 64, minlength=64).max() - 1
+        return tot / trials
+
+    wave_reads = (1024 + 94) / 64 * 8192
+    pred = extra(256, 4000) * wave_reads
+    assert abs(pred / 615682 - 1) < 0.03, pred
+    assert extra(16, 200) == 0

@@ -4,4 +4,5 @@
 cd ${GRAFT_REPO_ROOT:-.}
 tools/pmc.sh gpurun_out/r05h/pmc_c5h c5h && tools/pmc.sh gpurun_out/r05h/pmc_c5 c5 &&
 python3 tools/pmc_summary.py gpurun_out/r05h/pmc_c5h > gpurun_out/r05h/c5h_summary.txt &&
-python3 tools/pmc_summary.py gpurun_out/r05h/pmc_c5 > gpurun_out/r05h/c5_summary.txt
+python3 tools/pmc_summary.py gpurun_out/r05h/pmc_c5 > gpurun_out/r05h/c5_summary.txt &&
+timeout -k 10 120 tools/ubench/valu_rates > gpurun_out/r05h/valu_rates.txt 2>&1

@@ -78,6 +78,26 @@ __global__ void k_floor(float* o, float s) {
   }
   float t = 0; for (int i = 0; i < 16; ++i) t += a[i]; o[blockIdx.x * blockDim.x + threadIdx.x] = t;
 }
+// v_fma_mix_f32 with an f16 first source (the conversion folded into the FMA) and the plain
+// v_cvt_f32_f16 it would replace: issue cost of each (asm, so the forms are exactly these)
+__global__ void k_fmamix(float* o, float s) {
+  float a[16]; for (int i = 0; i < 16; ++i) a[i] = threadIdx.x + i;
+  const uint32_t h = 0x3c003c00u + threadIdx.x;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(a[i]) : "v"(h), "v"(s));
+  }
+  float t = 0; for (int i = 0; i < 16; ++i) t += a[i]; o[blockIdx.x * blockDim.x + threadIdx.x] = t;
+}
+__global__ void k_cvt(float* o, float s) {
+  float a[16]; uint32_t h[16];
+  for (int i = 0; i < 16; ++i) { a[i] = 0; h[i] = 0x3c003c00u + threadIdx.x + i; }
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("v_cvt_f32_f16 %0, %1" : "=v"(a[i]) : "v"(h[i]));
+  }
+  float t = 0; for (int i = 0; i < 16; ++i) t += a[i]; o[blockIdx.x * blockDim.x + threadIdx.x] = t;
+}
 template <typename F> double run(F f, const char* name, double ops_per_lane, int blocks, int threads) {
   float* o; hipMalloc(&o, (size_t)blocks * threads * 4);
   f(o); hipDeviceSynchronize();
@@ -102,6 +122,8 @@ int main() {
   run([&](float* o) { hipLaunchKernelGGL(k_fma, B, T, 0, 0, o, 0.999f); }, "v_fma_f32", ITERS * 16.0, B, T);
   run([&](float* o) { hipLaunchKernelGGL(k_pkfma, B, T, 0, 0, o, 0.999f); }, "v_pk_fma_f32", ITERS * 16.0, B, T);
   run([&](float* o) { hipLaunchKernelGGL(k_sin, B, T, 0, 0, o, 0.999f); }, "v_sin_f32", ITERS * 16.0, B, T);
+  run([&](float* o) { hipLaunchKernelGGL(k_fmamix, B, T, 0, 0, o, 0.999f); }, "v_fma_mix_f32 (f16 src0)", ITERS * 16.0, B, T);
+  run([&](float* o) { hipLaunchKernelGGL(k_cvt, B, T, 0, 0, o, 0.999f); }, "v_cvt_f32_f16", ITERS * 16.0, B, T);
   run([&](float* o) { hipLaunchKernelGGL(k_lds, B / 2, T, 0, 0, o, 1); }, "ds_read_b64 stride8B(+add)", ITERS * 16.0, B / 2, T);
   run([&](float* o) { hipLaunchKernelGGL(k_lds, B / 2, T, 0, 0, o, 2); }, "ds_read_b64 stride16B(+add)", ITERS * 16.0, B / 2, T);
   run([&](float* o) { hipLaunchKernelGGL(k_lds, B / 2, T, 0, 0, o, 5); }, "ds_read_b64 stride40B(+add)", ITERS * 16.0, B / 2, T);
