@@ -892,11 +892,18 @@ struct RxMfma {
                                 Walk& w, const Ctx& cx, QT (&pre)[UQ], ST& ps, int kpred) {
         const float sc = __builtin_ldexpf(1.0f, kpred);
         const cf2 win = window(kpred);
-        while (w.i < w.count) {
-            const int64_t t = w.t;
+        bool last = false;
+        __amdgpu_buffer_rsrc_t nxt;
+        // stage the tile at w.i (reloading the registers with the next tile's window) and check its
+        // votes: false = the general path redoes it. Called before the loop and at the end of its
+        // body, so that every path into the loop head has issued the staging's reloads last: with
+        // the staging at the head, the vote's exit and the loop's latch shared a block, and the
+        // compiler's wait tracking, merging a path without the tile's I/Q and decision stores,
+        // made each staging wait for the previous tile's stores to complete.
+        auto stage_tile = [&]() -> bool {
             const bool fi = w.full();
             const bool pf = w.next_full();
-            const __amdgpu_buffer_rsrc_t nxt = window_rsrc(p, pf ? w.q + w.dq : 0, pf);
+            nxt = window_rsrc(p, pf ? w.q + w.dq : 0, pf);
             const Idx ix = idx_split(p.c0 + (uint64_t)(w.q + p.n_start));
             // the staging (VALU-bound, the limiting stage) issues ahead of the other
             // workgroups' filter and stores on the SIMD: C3 RX 31.6-31.8 -> 31.0-31.4 us by
@@ -905,12 +912,20 @@ struct RxMfma {
             stage<SC>(p, pl, votes, ix, sc, win, pre, ps, nxt);
             __builtin_amdgcn_s_setprio(0);
             __syncthreads();
-            if (!(fi && fast_ok(votes, kpred))) return;
-            if (t == w.last && threadIdx.x == 0) *p.ka_out = kpred;   // the call's last tile
+            return fi && fast_ok(votes, kpred);
+        };
+        if (w.i >= w.count || !stage_tile()) return;
+        for (;;) {
+            const int64_t t = w.t;
+            last |= t == w.last;
             filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb, pre, &nxt);
             if (KS == 1) __syncthreads();      // the planes are restaged next (KS = 2: in filter_emit)
             w.next();
+            if (w.i >= w.count || !stage_tile()) break;
         }
+        // the call's last tile: its exponent is where the next call's prediction starts (stored
+        // after the loop: a store under a branch in it would break the wait tracking likewise)
+        if (last && threadIdx.x == 0) *p.ka_out = kpred;
     }
 
     // HO (the fused small call, modem_chain.hip): the tap tables are already in LDS, `ho.kin`

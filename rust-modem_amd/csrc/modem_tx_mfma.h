@@ -147,9 +147,12 @@ struct TxMfma {
     // (4 instead of 6 with a lo symbol plane).
     static constexpr bool HI = std::is_same<OutT, __half>::value;
 
-    // Raw bits word of symbol m, BPS bytes (fast path: aligned, no leftover bits).
+    // Raw bits word of symbol m, BPS bytes (fast path: aligned, no leftover bits), in 32 bits up to
+    // 4 bytes: held as 64 bits, a 1- or 2-byte word was masked (v_and) right after its load, which
+    // made the tile loop's bits prefetch wait for itself at once (BPSK, QPSK).
+    template <int BPS> using Word = typename std::conditional<BPS == 8, uint64_t, uint32_t>::type;
     template <int BPS>
-    __device__ static uint64_t load_word(const uint8_t* bits, int64_t m) {
+    __device__ static Word<BPS> load_word(const uint8_t* bits, int64_t m) {
         const uint8_t* b = bits + m * BPS;
         if (BPS == 1) return *b;
         if (BPS == 2) return *reinterpret_cast<const uint16_t*>(b);
@@ -259,7 +262,7 @@ struct TxMfma {
     // Full 16x16 tile, carrier index < 2^53: unconditional stores. jt = call sample index of
     // the sub-tile's first sample. Per sample: packed unscale (2^-kab), bit-exact phase,
     // sin/cos, packed mix; stores through a uniform base + 32-bit lane offsets.
-    template <bool RAW = false>
+    template <bool RAW = false, bool NT = false>
     __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale,
                                      const RawOut& ro = RawOut{}) {
         const int lane = threadIdx.x & 63;
@@ -296,21 +299,21 @@ struct TxMfma {
         // The sub-tile's 256 samples through a buffer descriptor at its wave-uniform first sample
         // (lane byte offsets < 256 samples): buffer stores count in vmcnt only (a store through a
         // generic pointer is a flat_store, also counted in lgkmcnt, and made every later LDS wait a
-        // wait for all the wave's sample stores), and the non-temporal policy is an immediate of
-        // the store, so the two forms below stay two instructions (as plain global stores under a
-        // uniform branch, the compiler merged them and dropped the non-temporal hint).
+        // wait for all the wave's sample stores). Every store here is unconditional and its cache
+        // policy (NT: non-temporal, past the Infinity Cache, tx_nt_below) a template constant: a
+        // store under a runtime branch (the policy, or the f16 form by the output's alignment) made
+        // the compiler's wait tracking lose count of the stores in the tile loop, so that each
+        // tile's staging waited for all of the previous tile's stores to complete.
         constexpr int SBYTES = (OUT_MODE == OUT_REAL ? 1 : 2) * (int)sizeof(OutT);
+        constexpr int POL = NT && OUT_MODE != OUT_REAL ? BUF_NT : BUF_DEFAULT;
         const __amdgpu_buffer_rsrc_t rs = buf_rsrc(reinterpret_cast<const char*>(p.out) + jt * SBYTES, 256 * SBYTES);
-        const bool nt = jt < p.nt_below;                    // uniform: past the Infinity Cache (tx_nt_below)
-        // f16 samples (4 B): a lane's one-sample stores would leave every 16-lane group
-        // writing half a 128-B line. Neighbour lanes swap one packed sample (DPP) so that the
-        // even lane holds samples i, i+1 of row r and the odd one samples i-1, i of row r+1:
-        // each 8-B store instruction then writes rows r and r+1 of the group, one whole line.
-        // Every such store lands at out + 8 k, so the form needs an 8-byte aligned first sample
-        // (uniform); a caller's f16 buffer that is only 4-byte aligned (a sliced (n, 2) tensor)
-        // or a sub-tile at an odd call sample takes the one-sample stores below.
-        const uint64_t oa = (uint64_t)p.out + (uint64_t)jt * SBYTES;
-        if (std::is_same<OutT, __half>::value && OUT_MODE != OUT_REAL && (oa & 7) == 0) {
+        if constexpr (std::is_same<OutT, __half>::value && OUT_MODE != OUT_REAL) {
+            // f16 samples (4 B): a lane's one-sample stores would leave every 16-lane group
+            // writing half a 128-B line. Neighbour lanes swap one packed sample (DPP) so that the
+            // even lane holds samples i, i+1 of row r and the odd one samples i-1, i of row r+1:
+            // each 8-B store instruction then writes rows r and r+1 of the group, one whole line.
+            // Every such store lands at out + 8 k: the caller guarantees an 8-byte aligned output
+            // (fast_ok; a 4-byte aligned f16 buffer, a sliced (n, 2) tensor, takes emit_edge).
             const bool odd = lane & 1;
 #pragma unroll
             for (int r = 0; r < 4; r += 2) {
@@ -319,8 +322,7 @@ struct TxMfma {
                 const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)(odd ? a : b), 0xB1, 0xF, 0xF, false);
                 const gv2u v = odd ? (gv2u){recv, b} : (gv2u){a, recv};
                 const int vo = (odd ? loff + 16 * (r + 1) - 1 : loff + 16 * r) * SBYTES;
-                if (nt) __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_NT);
-                else __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_DEFAULT);
+                __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, POL);
             }
         } else {
 #pragma unroll
@@ -328,21 +330,20 @@ struct TxMfma {
                 const int vo = (loff + 16 * r) * SBYTES;
                 if constexpr (OUT_MODE == OUT_REAL) {
                     if constexpr (std::is_same<OutT, float>::value)
-                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z[r].x), rs, vo, 0, BUF_DEFAULT);
+                        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, z[r].x), rs, vo, 0, POL);
                     else
-                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, __float2half_rn(z[r].x)), rs, vo, 0,
-                                                              BUF_DEFAULT);
-                } else if constexpr (std::is_same<OutT, float>::value) {
-                    const gv2u v = __builtin_bit_cast(gv2u, z[r]);
-                    if (nt) __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_NT);
-                    else __builtin_amdgcn_raw_buffer_store_b64(v, rs, vo, 0, BUF_DEFAULT);
+                        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, __float2half_rn(z[r].x)), rs, vo, 0, POL);
                 } else {
-                    const uint32_t v = __builtin_bit_cast(uint32_t, __floats2half2_rn(z[r].x, z[r].y));
-                    if (nt) __builtin_amdgcn_raw_buffer_store_b32(v, rs, vo, 0, BUF_NT);
-                    else __builtin_amdgcn_raw_buffer_store_b32(v, rs, vo, 0, BUF_DEFAULT);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gv2u, z[r]), rs, vo, 0, POL);
                 }
             }
         }
+    }
+
+    // The fast tile loop's precondition beyond the bits layout: an f16 output 8-byte aligned (its
+    // pair stores, emit_full; 8 | out + 4 * SPS * k for every sub-tile since SPS is even).
+    __device__ static bool out_ok(const TxParams& p) {
+        return !(std::is_same<OutT, __half>::value && OUT_MODE != OUT_REAL) || ((uintptr_t)p.out & 7) == 0;
     }
 
     // Partial tile, samples before the call, or carrier index >= 2^53: guarded, 64-bit
@@ -496,7 +497,7 @@ struct TxMfma {
             const int64_t ms = t * TS - lead - PRE;
             return BPS > 0 && ms >= 0 && ms + NE <= p.nsym_valid && t * TS - lead + TS <= p.nsym;
         };
-        uint64_t pre[U];
+        Word<BPS> pre[U];
         auto prefetch = [&](int64_t t) {
             const int64_t ms = t * TS - lead - PRE;
 #pragma unroll
@@ -519,7 +520,14 @@ struct TxMfma {
             if (full(t)) {
                 if (!ready) prefetch(t);
                 ready = false;
-                for (; t < t1 && full(t); t += ts) {
+                // the first tile's bits complete before the loop: a load still pending on entry
+                // merged into the loop head's wait tracking
+#pragma unroll
+                for (int u = 0; u < U; ++u) asm volatile("" ::"v"(pre[u]));
+                // one full tile; NTT: its stores non-temporal (below tx_nt_below), a template
+                // constant per loop so that no store sits under a runtime branch (emit_full)
+                auto tile = [&](auto ntc) {
+                    constexpr bool NTT = decltype(ntc)::value;
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const int e = tid + NT * u;
@@ -537,11 +545,14 @@ struct TxMfma {
                         // of the other workgroups' staging and filter: +0.6 % C3 bench in
                         // three interleaved pairs (profiles/r02_store_layout_ab.txt)
                         __builtin_amdgcn_s_setprio(1);
-                        emit_full(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
+                        emit_full<false, NTT>(p, j0 + ((int64_t)(wave * SUB + q) * 16 * SB) * SPS, dre, dim, unscale);
                         __builtin_amdgcn_s_setprio(0);
                     }
                     __syncthreads();                     // the window is restaged next trip
-                }
+                };
+                // tiles walk upwards: those wholly below tx_nt_below come first
+                for (; t < t1 && full(t) && (t * TS - lead + TS) * SPS <= p.nt_below; t += ts) tile(std::true_type{});
+                for (; t < t1 && full(t); t += ts) tile(std::false_type{});
             } else {
                 stage_slow(p, pl, lut_s, t * TS - lead - PRE);
                 __syncthreads();
@@ -600,7 +611,7 @@ __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __res
     // (measured 1 % faster on C3 than contiguous ranges per workgroup)
     const int64_t t0 = bid, t1 = ntiles, ts = nb;
     if (t0 >= t1) return;
-    if (p.fast_bits && p.exact_idx) {              // one uniform switch: the tile loop is specialised
+    if (p.fast_bits && p.exact_idx && K::out_ok(p)) {   // one uniform switch: the tile loop is specialised
         switch (p.bps) {
         case 1: K::template run<1>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
         case 2: K::template run<2>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
