@@ -539,8 +539,9 @@ struct RxMfma {
         }
     }
 
-    // The tile's matched filter and outputs (instants ot0 + 256 blk ..). KS = 1: waves < NWF
-    // filter their block and store. KS = 2: waves blk and blk + NWF each sum half of block blk's
+    // The tile's matched filter and outputs (instants ot0 + 256 blk ..); returns with the planes
+    // free for the next staging. KS = 1: waves < NWF filter their block, a barrier, then they store.
+    // KS = 2: waves blk and blk + NWF each sum half of block blk's
     // k-steps (the same two halves fir adds); the upper wave hands its sums over in LDS before a
     // barrier, after which the planes may be restaged, and the lower wave adds them and stores.
     template <int EM>
@@ -550,7 +551,8 @@ struct RxMfma {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         f32x4 dre, dim;
         if constexpr (KS == 1) {
-            if (NWF == NW || wave < NWF) {     // uniform
+            const bool fw = NWF == NW || wave < NWF;   // uniform
+            if (fw) {
                 fir(pl, tbl, dre, dim);
                 if (LATE > 0 && pre) {         // the late slots' reloads (see LATE)
                     __builtin_amdgcn_sched_barrier(0);
@@ -559,8 +561,11 @@ struct RxMfma {
                     for (int u = UQ - LATE; u < UQ; ++u) pre[u] = load_slot(*nxt, voff, u);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                emit<EM>(p, ot0 + wave * 256, dre, dim, kab);
             }
+            // the planes are free once every wave has filtered: the outputs (slicer, stores) of
+            // a wave that is done overlap the other waves' filters and the next tile's staging
+            __syncthreads();
+            if (fw) emit<EM>(p, ot0 + wave * 256, dre, dim, kab);
         } else {
             const int blk = wave % NWF, kh = wave / NWF;
             fir_part<NKS / 2>(pl, tbl, blk, kh * (NKS / 2), dre, dim);
@@ -572,8 +577,12 @@ struct RxMfma {
             if (kh == 0) {
                 dre += *pr;
                 dim += *pi;
-                emit<EM>(p, ot0 + blk * 256, dre, dim, kab);
             }
+            // every wave issues the stores, the upper ones past the call's last instant (their
+            // descriptors hold no records: dropped), so that no store sits under a branch in the
+            // tile loop (the compiler's wait tracking then lost count of them: each staging waited
+            // for the previous tile's stores)
+            emit<EM>(p, kh == 0 ? ot0 + blk * 256 : p.nout, dre, dim, kab);
         }
     }
 
@@ -835,8 +844,7 @@ struct RxMfma {
             put4(pl, ppos(e0), a, b);
         }
         __syncthreads();
-        filter_emit<EM>(p, pl, tbl, part, t * TS - ld, ka + kb);
-        __syncthreads();                       // the planes are restaged next
+        filter_emit<EM>(p, pl, tbl, part, t * TS - ld, ka + kb);   // ends with the planes free
         return ka;
     }
 
@@ -918,8 +926,7 @@ struct RxMfma {
         for (;;) {
             const int64_t t = w.t;
             last |= t == w.last;
-            filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb, pre, &nxt);
-            if (KS == 1) __syncthreads();      // the planes are restaged next (KS = 2: in filter_emit)
+            filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb, pre, &nxt);   // planes free after it
             w.next();
             if (w.i >= w.count || !stage_tile()) break;
         }
