@@ -171,6 +171,23 @@ struct TxMfma {
         }
     }
 
+    // The tile's symbols from the prefetched bits words: every slot's LUT entry read first, then the
+    // plane writes (one LDS round trip for all slots; per slot, each write waited for its own read).
+    // Slots wholly inside the window need no guard: only the last can reach past it (its clamped
+    // word still indexes the LUT).
+    template <int BPS>
+    __device__ __forceinline__ static void put_all(_Float16* pl, const th4* lut_s, const Word<BPS> (&pre)[U]) {
+        const int tid = threadIdx.x;
+        th4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = lut_s[word_index(pre[u], BPS)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = tid + NT * u;
+            if ((u + 1) * NT <= NE || e < NE) put(pl, e, v[u]);
+        }
+    }
+
     // f32 symbol value -> scaled (2^ka) split halves (re_hi, re_lo, im_hi, im_lo), as the host
     // splits the LUT (round to nearest both times).
     __device__ static th4 split_value(const TxParams& p, float2 v) {
@@ -413,7 +430,7 @@ struct TxMfma {
         const cf2 unscale = {us, us};
         const int64_t ms = t * TS - p.lead - PRE, mlast = p.nsym_valid - 1;
         const bool fullt = BPS > 0 && ms >= 0 && ms + NE <= p.nsym_valid && t * TS - p.lead + TS <= p.nsym;
-        uint64_t pre[U];
+        Word<BPS> pre[U];
         if (fullt) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -442,11 +459,7 @@ struct TxMfma {
         for (int i = tid; i < (1 << p.bps); i += NT) lut_s[i] = lut_h[i];
         __syncthreads();   // LUT visible
         if (fullt) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int e = tid + NT * u;
-                if (e < NE) put(pl, e, lut_s[word_index(pre[u], BPS)]);
-            }
+            put_all<BPS>(pl, lut_s, pre);
         } else {
             stage_slow(p, pl, lut_s, ms);
         }
@@ -528,11 +541,7 @@ struct TxMfma {
                 // constant per loop so that no store sits under a runtime branch (emit_full)
                 auto tile = [&](auto ntc) {
                     constexpr bool NTT = decltype(ntc)::value;
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const int e = tid + NT * u;
-                        if (e < NE) put(pl, e, lut_s[word_index(pre[u], BPS)]);
-                    }
+                    put_all<BPS>(pl, lut_s, pre);
                     __syncthreads();
                     if (t + ts < t1) prefetch(t + ts);   // next bits fly during the MFMAs
                     const int64_t j0 = (t * TS - lead) * SPS;
