@@ -137,7 +137,9 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
         }
         if (!done) TK::template one_tile<0>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro);
         // TX tiles past the last RX tile (their samples only feed the RX history)
+#ifndef MODEM_CHAIN_NOTAIL      // timing probe only (A/B builds): the last workgroup's extra work skipped
         if (bid == nb - 1 && g.ntx > g.nrx) TK::template run<0>(tp, pl, lut_s, bh, bl, g.nrx, g.ntx, 1, 0);
+#endif
     }
     _Float16* tbl = lds_s + L::TBL;
 #pragma unroll
@@ -145,11 +147,13 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
         const int j = threadIdx.x + k * 256;
         if (j < RK::K_TAB8) reinterpret_cast<h8*>(tbl)[j] = tv[k];
     }
+#ifndef MODEM_CHAIN_NOTAIL
     if (bid == nb - 1) {                       // the RX history reads HBM: this workgroup's stores first
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         rx_state_update<float>(rp);
     }
+#endif
     const TileSeq sq{t, -1, 1, g.nrx};
     RK::template run<EM, true>(rp, lds_s, tbl, tables, reinterpret_cast<float*>(lds_s + L::RED), sq, bid,
                                RxHandoff{raw, rb, rn, kin});
