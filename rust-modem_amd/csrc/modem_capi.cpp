@@ -348,6 +348,7 @@ struct modem_tx {
     float ph_amp = 0.f, ph_freq = 0.f, ph_shift = 0.f, ph_max = 0.f;
     int ph_spb = 0, ph_map = 0;
     Stage scan_stage;               // per-symbol states of the scanned phasors
+    Stage batch_params;             // a scan batch's parameter blocks, when this is its first handle
     float2* d_hist[2] = {nullptr, nullptr};
     uint8_t* d_carry[2] = {nullptr, nullptr};
     int hcur = 0, ccur = 0, ncarry = 0;
@@ -702,6 +703,46 @@ modem_status modem_tx_process(modem_tx* h, const uint8_t* bits, size_t nbits, vo
 modem_status modem_tx_flush(modem_tx* h, void* out, size_t cap, size_t* produced, void* stream) {
     return tx_run(h, nullptr, 0, true, out, cap, produced, (hipStream_t)stream);
 }
+// Channels of one scanned phasor kind (DMPSK / MFSK / BFSK; modem_tx_process_batch): their serial
+// symbol-state scans run as one launch, one lane per channel (tx_scan_batch: each channel's
+// states bit for bit those of its single call), then each channel's sample kernel. Every buffer is
+// device memory; the handles are distinct and share a device.
+static modem_status tx_scan_batch_run(modem_tx* const* hs, size_t nch, const uint8_t* const* bits,
+                                      const size_t* nbits, void* const* outs, const size_t* caps, size_t* produced,
+                                      hipStream_t s) {
+    std::vector<int64_t> nsym(nch);
+    std::vector<int> ncarry_new(nch);
+    for (size_t c = 0; c < nch; ++c) {        // every channel's size first: an error leaves the handles untouched
+        const modem_tx* h = hs[c];
+        const uint64_t total = (uint64_t)h->ncarry + nbits[c];
+        nsym[c] = (int64_t)(total / h->bps);
+        ncarry_new[c] = (int)(total - (uint64_t)nsym[c] * h->bps);
+        if ((size_t)nsym[c] * h->sps > caps[c]) return MODEM_ERR_CAPACITY;
+    }
+    DeviceGuard g(hs[0]->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    modem_status st;
+    std::vector<mk::TxParams> ps(nch);
+    for (size_t c = 0; c < nch; ++c) {
+        modem_tx* h = hs[c];
+        if ((st = h->scan_stage.ensure((size_t)std::max<int64_t>(nsym[c], 1) * sizeof(float2)))) return st;
+        tx_fill(h, bits[c], nbits[c], false, outs[c], nsym[c], ncarry_new[c], (size_t)nsym[c] * h->sps, ps[c]);
+        ps[c].scan = static_cast<float2*>(h->scan_stage.p);
+    }
+    if ((st = hs[0]->batch_params.ensure(nch * sizeof(mk::TxParams)))) return st;
+    // (from pageable host memory: synchronous, so `ps` may go when the call returns)
+    HIP_TRY(hipMemcpyAsync(hs[0]->batch_params.p, ps.data(), nch * sizeof(mk::TxParams), hipMemcpyHostToDevice, s));
+    HIP_TRY(mk::launch_tx_scan_batch(static_cast<const mk::TxParams*>(hs[0]->batch_params.p), (int)nch,
+                                      hs[0]->ph_kind, s));
+    for (size_t c = 0; c < nch; ++c) {
+        modem_tx* h = hs[c];
+        HIP_TRY(mk::launch_tx_phasor(ps[c], h->dtype, h->out_mode, s, true));
+        tx_advance(h, false, nsym[c], ncarry_new[c], (size_t)nsym[c] * h->sps);
+        produced[c] = (size_t)nsym[c] * h->sps;
+    }
+    return MODEM_OK;
+}
+
 // One launch for several channels (independent channel streams). Equivalent to
 // modem_tx_process(hs[c], bits[c], nbits[c], outs[c], caps[c], &produced[c], stream) for
 // c = 0 .. nch-1 in order; fused into one launch per kBatchMax channels when every handle
@@ -716,6 +757,17 @@ modem_status modem_tx_process_batch(modem_tx* const* hs, size_t nch, const uint8
     for (size_t c = 0; c < nch; ++c)    // an error leaves every handle untouched
         if (hs[c] && ((nbits[c] && foreign_ptr(bits[c], hs[c]->device)) || foreign_ptr(outs[c], hs[c]->device)))
             return MODEM_ERR_INVALID_ARG;
+    bool scan = nch >= 2 && hs[0] != nullptr && phasor_scanned(hs[0]->ph_kind);
+    for (size_t c = 0; scan && c < nch; ++c) {
+        const modem_tx* h = hs[c];
+        scan = h && h->device == hs[0]->device && h->ph_kind == hs[0]->ph_kind &&
+               (nbits[c] == 0 || (bits[c] && is_device_ptr(bits[c]))) && outs[c] && is_device_ptr(outs[c]);
+        for (size_t e = 0; scan && e < c; ++e) scan = hs[e] != h;      // a handle at most once
+    }
+    if (scan) {
+        for (size_t c = 0; c < nch; ++c) produced[c] = 0;
+        return tx_scan_batch_run(hs, nch, bits, nbits, outs, caps, produced, s);
+    }
     bool fuse = nch >= 2 && hs[0] != nullptr;
     for (size_t c = 0; fuse && c < nch; ++c) {
         const modem_tx* h = hs[c];
@@ -1211,6 +1263,7 @@ struct modem_chain_batch {
     // MODEM_CHAIN_BATCH_LANES=1 in the environment at create time: one lane.
     hipStream_t side = nullptr;
     hipEvent_t ev_start = nullptr, ev_end = nullptr;
+    bool failed = false;                // a launch of a run failed (modem_chain_batch_run)
     ~modem_chain_batch() {
         if (ev_start) (void)hipEventDestroy(ev_start);
         if (ev_end) (void)hipEventDestroy(ev_end);
@@ -1282,28 +1335,11 @@ modem_status modem_chain_batch_create(modem_tx* const* txs, modem_rx* const* rxs
     return MODEM_OK;
 }
 
-modem_status modem_chain_batch_run(modem_chain_batch* b, size_t* produced, size_t* produced_out, void* stream) {
-    if (!b) return MODEM_ERR_INVALID_ARG;
+// The launches of one run, group by group (after the checks of modem_chain_batch_run).
+static modem_status chain_batch_launch(modem_chain_batch* b, hipStream_t s, size_t* produced, size_t* produced_out) {
     const size_t nch = b->tx.size();
-    const hipStream_t s = (hipStream_t)stream;
-    // every channel's call sizes first: an error leaves every handle untouched
     int64_t nsym[mk::kBatchMax], k_first[mk::kBatchMax], nout[mk::kBatchMax];
     int ncarry_new[mk::kBatchMax];
-    for (size_t c = 0; c < nch; ++c) {
-        const modem_tx* t = b->tx[c];
-        const uint64_t total = (uint64_t)t->ncarry + b->nbits[c];
-        const int64_t ns = (int64_t)(total / t->bps);
-        if ((size_t)ns * t->sps > b->caps[c]) return MODEM_ERR_CAPACITY;
-        int64_t k0, k;
-        rx_range(b->rx[c]->consumed, b->rx[c]->consumed + ns * (int64_t)t->sps, b->rx[c]->decim, b->rx[c]->D, &k0, &k);
-        if ((size_t)k > b->out_caps[c]) return MODEM_ERR_CAPACITY;
-    }
-    DeviceGuard g(b->tx[0]->device);
-    if (!g.ok) return MODEM_ERR_NO_DEVICE;
-    if (b->side) {                              // the plan's lane starts after what precedes the run
-        HIP_TRY(hipEventRecord(b->ev_start, s));
-        HIP_TRY(hipStreamWaitEvent(b->side, b->ev_start, 0));
-    }
     for (size_t c0 = 0; c0 < nch; c0 += b->group) {
         const int n = (int)std::min(b->group, nch - c0);
         const hipStream_t ls = b->side && (c0 / b->group) % 2 ? b->side : s;   // this group's lane
@@ -1341,11 +1377,42 @@ modem_status modem_chain_batch_run(modem_chain_batch* b, size_t* produced, size_
         HIP_TRY(mk::launch_rx_mfma_batch(rb, (int)r0->decim, r0->mfma_ksteps, r0->d_bfrag, r0->in_dtype, ls));
         for (int i = 0; i < n; ++i) rx_advance(b->rx[c0 + i], (size_t)nsym[i] * b->tx[c0 + i]->sps);
     }
-    if (b->side) {                              // and the caller's stream continues after both lanes
-        HIP_TRY(hipEventRecord(b->ev_end, b->side));
-        HIP_TRY(hipStreamWaitEvent(s, b->ev_end, 0));
-    }
     return MODEM_OK;
+}
+
+modem_status modem_chain_batch_run(modem_chain_batch* b, size_t* produced, size_t* produced_out, void* stream) {
+    if (!b) return MODEM_ERR_INVALID_ARG;
+    // a launch failed in an earlier run: some groups' handles advanced and others not, so the
+    // channels' streams no longer line up (the plan and its handles are unusable)
+    if (b->failed) return MODEM_ERR_HIP;
+    const size_t nch = b->tx.size();
+    const hipStream_t s = (hipStream_t)stream;
+    // every channel's call sizes first: an error here leaves every handle untouched
+    for (size_t c = 0; c < nch; ++c) {
+        const modem_tx* t = b->tx[c];
+        const uint64_t total = (uint64_t)t->ncarry + b->nbits[c];
+        const int64_t ns = (int64_t)(total / t->bps);
+        if ((size_t)ns * t->sps > b->caps[c]) return MODEM_ERR_CAPACITY;
+        int64_t k0, k;
+        rx_range(b->rx[c]->consumed, b->rx[c]->consumed + ns * (int64_t)t->sps, b->rx[c]->decim, b->rx[c]->D, &k0, &k);
+        if ((size_t)k > b->out_caps[c]) return MODEM_ERR_CAPACITY;
+    }
+    DeviceGuard g(b->tx[0]->device);
+    if (!g.ok) return MODEM_ERR_NO_DEVICE;
+    if (b->side) {                              // the plan's lane starts after what precedes the run
+        HIP_TRY(hipEventRecord(b->ev_start, s));
+        HIP_TRY(hipStreamWaitEvent(b->side, b->ev_start, 0));
+    }
+    const modem_status st = chain_batch_launch(b, s, produced, produced_out);
+    if (b->side) {                              // the caller's stream continues after both lanes:
+        // also after a failed launch (best effort), so that the caller's stream is still ordered
+        // after the side lane's kernels already queued
+        const bool joined = hipEventRecord(b->ev_end, b->side) == hipSuccess &&
+                            hipStreamWaitEvent(s, b->ev_end, 0) == hipSuccess;
+        if (st == MODEM_OK && !joined) { (void)hipGetLastError(); b->failed = true; return MODEM_ERR_HIP; }
+    }
+    if (st != MODEM_OK) b->failed = true;
+    return st;
 }
 
 modem_status modem_chain_batch_destroy(modem_chain_batch* b) { delete b; return MODEM_OK; }

@@ -137,9 +137,7 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
         }
         if (!done) TK::template one_tile<0>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro);
         // TX tiles past the last RX tile (their samples only feed the RX history)
-#ifndef MODEM_CHAIN_NOTAIL      // timing probe only (A/B builds): the last workgroup's extra work skipped
         if (bid == nb - 1 && g.ntx > g.nrx) TK::template run<0>(tp, pl, lut_s, bh, bl, g.nrx, g.ntx, 1, 0);
-#endif
     }
     _Float16* tbl = lds_s + L::TBL;
 #pragma unroll
@@ -147,13 +145,11 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
         const int j = threadIdx.x + k * 256;
         if (j < RK::K_TAB8) reinterpret_cast<h8*>(tbl)[j] = tv[k];
     }
-#ifndef MODEM_CHAIN_NOTAIL
     if (bid == nb - 1) {                       // the RX history reads HBM: this workgroup's stores first
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         rx_state_update<float>(rp);
     }
-#endif
     const TileSeq sq{t, -1, 1, g.nrx};
     RK::template run<EM, true>(rp, lds_s, tbl, tables, reinterpret_cast<float*>(lds_s + L::RED), sq, bid,
                                RxHandoff{raw, rb, rn, kin});
@@ -180,7 +176,7 @@ static bool chain_geo(const TxParams& tp, const RxParams& rp, int64_t grid, Chai
     const int64_t tx0 = -(int64_t)tp.lead * SPS;                                   // TX tile 0's first sample
     const int64_t H = tx0 - q0;                                                    // window samples before it
     g.xs = H > 0 ? (int32_t)((H + SUBS - 1) / SUBS) : 0;
-    if (g.xs > 4 * SUB || q0 + RK::NS > tx0 + RXS) return false;
+    if (g.xs > 4 * TK::SUB || q0 + RK::NS > tx0 + RXS) return false;
     if (grid < 1 || grid > g.nrx) return false;
     const int64_t rl = g.nrx * (grid - 1) / grid;                                  // the last workgroup's first RX tile
     const int64_t own = tx0 + rl * RXS - (rl > 0 ? g.xs * SUBS : 0);               // its first written sample
@@ -275,11 +271,7 @@ hipError_t launch_chain_mfma(const TxParams& tp, int sps, int nks_t, const void*
 #undef CHN
         return hipErrorNotSupported;
     };
-#ifdef MODEM_DEV_MIN
-    const hipError_t e = dtype != 0 ? hipErrorNotSupported : sel(float());
-#else
     const hipError_t e = dtype == 1 ? sel(__half()) : sel(float());
-#endif
     if (form) *form = g_chain_form;
     return e;
 }

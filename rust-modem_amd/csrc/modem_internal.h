@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 
 namespace mk {
 
@@ -118,7 +119,11 @@ struct FirParams {
 hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s);
 // Sample-dependent phasors (DCQPSK, CPFSK, MSK; DMPSK, MFSK, BFSK after a serial symbol-state
 // scan), sample-and-hold: tx_scan + tx_phasor.
-hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s);
+// scanned: the states are already in p.scan (a batch's tx_scan_batch ran), only tx_phasor runs.
+hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s, bool scanned = false);
+// The serial state scan of DMPSK / MFSK / BFSK for nch channels of one phasor kind at once, one
+// lane per channel (dps: their TxParams in device memory, p.scan set).
+hipError_t launch_tx_scan_batch(const TxParams* dps, int nch, int kind, hipStream_t s);
 // TX FIR on the matrix cores (tx_mfma, split-f16 MFMA): 32-symbol k-steps for (sps, K), or 0
 // when no variant fits; bfrag = per-lane B fragments [ksteps][hi, lo][64 lanes][8 halves].
 int tx_mfma_ksteps(int sps, int K);
@@ -126,8 +131,15 @@ int tx_mfma_ksteps(int sps, int K);
 // independent handles of one configuration in one launch; the launcher sets g, the
 // workgroups per channel (workgroup b serves channel b / g).
 constexpr int kBatchMax = 8;
-struct TxBatch { TxParams p[kBatchMax]; int32_t nch; int32_t g; };
-struct RxBatch { RxParams p[kBatchMax]; int32_t nch; int32_t g; };
+struct TxBatch { TxParams p[kBatchMax]; int32_t nch; int32_t g; int32_t rot; };
+struct RxBatch { RxParams p[kBatchMax]; int32_t nch; int32_t g; int32_t rot; };
+// The per-channel rotation of a batch launch's workgroups (a multiple of 8, so that every tile
+// keeps its XCD slot: blocks b and b + 8 share an XCD); 0 when g is not a multiple of 8.
+// MODEM_BATCH_ROT=0 in the environment turns it off (A/B).
+inline int32_t batch_rot(int32_t g, int32_t nch) {
+    static const bool on = [] { const char* e = std::getenv("MODEM_BATCH_ROT"); return !e || e[0] != '0'; }();
+    return on && g % 8 == 0 && 8 * (nch - 1) < g ? 8 : 0;
+}
 // mixed-carrier I/Q output only (OUT_IQ_MIXED); dtype 0 f32, 1 f16
 hipError_t launch_tx_mfma_batch(const TxBatch& b, int sps, int nks, const void* bfrag, int dtype, hipStream_t s);
 // complex mix only (MIX_COMPLEX); in and out of one dtype
@@ -161,6 +173,18 @@ hipError_t launch_rx(const RxParams& p, int decim, int in_dtype, int out_dtype, 
 // *form = 1 (chain_mfma) or 2 (chain_small: one RX tile per workgroup, LDS hand-off).
 hipError_t launch_chain_mfma(const TxParams& tp, int sps, int nks_t, const void* bfrag, const RxParams& rp,
                              int nks_r, const void* tables, int dtype, hipStream_t s, int* form);
+// The matrix-core variants by element types, instantiated in their own translation units
+// (modem_txm_*.hip: OM = OUT_IQ_MIXED / BASEBAND / REAL, OutT = float / __half; modem_rxm_*.hip:
+// MIX = MIX_COMPLEX / MIX_REFERENCE_REAL, InT, OutT = float / __half) and dispatched from
+// launch_tx_mfma* / launch_rx_mfma* (hipErrorInvalidValue: no variant for the shape).
+template <int OM, typename OutT>
+hipError_t txm_sel(const TxParams& p, int sps, int nks, const void* bfrag, hipStream_t s);
+template <typename OutT>
+hipError_t txm_sel_batch(const TxBatch& b, int sps, int nks, const void* bfrag, hipStream_t s);
+template <typename InT, int MIX, typename OutT>
+hipError_t rxm_sel(const RxParams& p, int decim, int nks, const void* tables, hipStream_t s);
+template <typename T>
+hipError_t rxm_sel_batch(const RxBatch& b, int decim, int nks, const void* tables, hipStream_t s);
 hipError_t launch_fir(const FirParams& p, hipStream_t s);
 hipError_t launch_phases(float w, uint64_t s0, size_t n, float* out, hipStream_t s);
 hipError_t launch_prng_bits(uint64_t seed, uint8_t* out, size_t nbits, hipStream_t s);

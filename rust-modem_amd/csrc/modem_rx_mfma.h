@@ -366,20 +366,11 @@ struct RxMfma {
     // (the matched filter then single-buffers its operands to fit 128 VGPRs), else the
     // compiler's choice.
     static constexpr int WPE = SWZ && (LDS_BYTES <= 40960 || KS == 2) ? 4 : 1;
-#ifndef MODEM_RX_LATE
-#define MODEM_RX_LATE 0
-#endif
-#ifndef MODEM_RX_DB
-#define MODEM_RX_DB 0
-#endif
-#ifndef MODEM_RX_HI_NOLO       // experiment: f16 in and out, the taps' f16 roundings only
-#define MODEM_RX_HI_NOLO 0
-#endif
-    // LATE: the last LATE quad slots of a 1024-instant tile are reloaded with the next tile's
-    // samples after the matched filter instead of during the staging, so that their registers are
-    // free while the filter runs (DBF: it then double-buffers its operands at 4 waves per SIMD).
-    static constexpr int LATE = NWF == 4 && KS == 1 && WPE == 4 ? MODEM_RX_LATE : 0;
-    static constexpr bool DBF = WPE < 4 || (NWF == 4 && KS == 1 && MODEM_RX_DB);
+    // WPE 4: the matched filter single-buffers its operands (one k-step's at a time) to fit 128
+    // VGPRs; the other waves hide the LDS latency (double-buffered at 4 waves per SIMD, with the
+    // last slots' reloads moved after the filter to free their registers: neutral on C3, slower
+    // on C5 f16, profiles/r05_tx_wide.txt, r05_c2_floor_and_db.txt).
+    static constexpr bool DBF = WPE < 4;
     static_assert((4 * NT) % RW == 0, "a staging slot spans whole rows");
     // plane offset between staging slots (the swizzle repeats every 1024 samples)
     static constexpr int SLOT_POS = SWZ ? 4 * NT : 4 * NT + 16 * (4 * NT / RW);
@@ -443,11 +434,16 @@ struct RxMfma {
     // first sample and whose size is what of its 4 * NQ samples lies in the chunk (0 bytes: no
     // next tile). Loads past the size return zeros without touching memory (the spare lanes of
     // the last slot; a call's last tile; a workgroup's last tile), so the reload of every slot
-    // is unconditional.
+    // is unconditional. The descriptor never reaches outside the call's buffer: only tiles whose
+    // window starts inside the chunk take this path (Walk::nfull), and a window starting before
+    // it (q_lo < 0, which a misclassified tile would have: round 5's forced-fast-path build read
+    // before p.x and faulted) gets no records at all, so that its loads return zeros.
     __device__ static __amdgpu_buffer_rsrc_t window_rsrc(const RxParams& p, int64_t q_lo, bool live) {
         constexpr int S = sizeof(InT) * 2;
-        const uint32_t w = clamp64_u32(p.N - q_lo, (uint32_t)(4 * NQ));
-        return buf_rsrc(reinterpret_cast<const char*>(p.x) + q_lo * S, live ? w * (uint32_t)S : 0u);
+        const bool in = live && (int32_t)((uint64_t)q_lo >> 32) >= 0;     // q_lo >= 0, on 32-bit halves
+        const int64_t qb = in ? q_lo : 0;
+        const uint32_t w = clamp64_u32(p.N - qb, (uint32_t)(4 * NQ));
+        return buf_rsrc(reinterpret_cast<const char*>(p.x) + qb * S, in ? w * (uint32_t)S : 0u);
     }
     // P1: lane tid's sample of the partial slot (window sample 4 NT (U - 1) + tid)
     __device__ static ST load_one(__amdgpu_buffer_rsrc_t r, int tid) {
@@ -512,10 +508,8 @@ struct RxMfma {
             else if (s + 1 < NS_) load(s + 1, c ^ 1);
             r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][0], r0, 0, 0, 0);
             m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][0], m0, 0, 0, 0);
-            if (!(HI && MODEM_RX_HI_NOLO)) {
-                r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
-                m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][1], m0, 0, 0, 0);
-            }
+            r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][0], b[c][1], r0, 0, 0, 0);
+            m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][2], b[c][1], m0, 0, 0, 0);
             if (!HI) {
                 r0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][1], b[c][0], r0, 0, 0, 0);
                 m0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[c][3], b[c][0], m0, 0, 0, 0);
@@ -546,22 +540,12 @@ struct RxMfma {
     // barrier, after which the planes may be restaged, and the lower wave adds them and stores.
     template <int EM>
     __device__ __forceinline__ static void filter_emit(const RxParams& p, const _Float16* pl, const _Float16* tbl,
-                                                       f32x4* part, int64_t ot0, int kab, QT* pre = nullptr,
-                                                       const __amdgpu_buffer_rsrc_t* nxt = nullptr) {
+                                                       f32x4* part, int64_t ot0, int kab) {
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
         f32x4 dre, dim;
         if constexpr (KS == 1) {
             const bool fw = NWF == NW || wave < NWF;   // uniform
-            if (fw) {
-                fir(pl, tbl, dre, dim);
-                if (LATE > 0 && pre) {         // the late slots' reloads (see LATE)
-                    __builtin_amdgcn_sched_barrier(0);
-                    const int voff = 4 * tid_() * (int)sizeof(InT) * 2;
-#pragma unroll
-                    for (int u = UQ - LATE; u < UQ; ++u) pre[u] = load_slot(*nxt, voff, u);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
+            if (fw) fir(pl, tbl, dre, dim);
             // the planes are free once every wave has filtered: the outputs (slicer, stores) of
             // a wave that is done overlap the other waves' filters and the next tile's staging
             __syncthreads();
@@ -582,7 +566,8 @@ struct RxMfma {
             // descriptors hold no records: dropped), so that no store sits under a branch in the
             // tile loop (the compiler's wait tracking then lost count of them: each staging waited
             // for the previous tile's stores)
-            emit<EM>(p, kh == 0 ? ot0 + blk * 256 : p.nout, dre, dim, kab);
+            // (the upper waves skip the LUT slicer's search: its decisions are dropped anyway)
+            emit<EM>(p, kh == 0 ? ot0 + blk * 256 : p.nout, dre, dim, kab, kh != 0);
         }
     }
 
@@ -652,7 +637,7 @@ struct RxMfma {
             if ((u + 1) * 4 * NT <= NS || e0 < NS) put4(pl, pos0 + u * SLOT_POS, zr, zi);
             // (not hoisted above the mix: the slot's registers would be copied out first)
             __builtin_amdgcn_sched_barrier(0);
-            if (u < UQ - LATE) pre[u] = load_slot(nxt, voff, u);   // the next tile's slot u, same registers
+            pre[u] = load_slot(nxt, voff, u);   // the next tile's slot u, same registers
             __builtin_amdgcn_sched_barrier(0);                 // one quad's temporaries at a time
         }
         if constexpr (P1) {                    // the partial slot, one sample per lane: the quad path's
@@ -692,8 +677,11 @@ struct RxMfma {
     // through buffer descriptors over the wave's instants that are in the call: those before
     // the call's first (ot < 0: a lane offset below the base wraps out of range) and past its
     // last are dropped without a branch.
+    // dead (wave-uniform): every store of the wave lies past the call (the K-split's upper waves),
+    // so the LUT slicer's search is skipped; the stores themselves stay unconditional.
     template <int EM>
-    __device__ static void emit(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab) {
+    __device__ static void emit(const RxParams& p, int64_t ot, const f32x4& dre, const f32x4& dim, int kab,
+                                bool dead = false) {
         const int lane = tid_() & 63;
         if (EM == RXE_GEN) {                   // any other output combination: guarded stores
 #pragma unroll
@@ -727,6 +715,7 @@ struct RxMfma {
             }
             if (EM & RXE_SYM) {
                 const uint8_t sy = !(EM & RXE_NEAREST) ? rx_slice_qam2(p, a, b)
+                                 : dead ? (uint8_t)0
                                  : p.bps == 2 ? rx_slice_nearest4(p, a, b) : rx_slice_nearest(p, a, b);
                 __builtin_amdgcn_raw_buffer_store_b8(sy, rsy, off, 0, 0);
             }
@@ -926,7 +915,7 @@ struct RxMfma {
         for (;;) {
             const int64_t t = w.t;
             last |= t == w.last;
-            filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb, pre, &nxt);   // planes free after it
+            filter_emit<EM>(p, pl, tbl, part, t * TS - cx.ld, kpred + cx.kb);   // planes free after it
             w.next();
             if (w.i >= w.count || !stage_tile()) break;
         }

@@ -11,6 +11,7 @@
 //        bit-exact carrier phase (carrier.rs:17-19, util.rs:3-6), mixes (i+jq)e^{j phase}
 //        and writes 16-B coalesced stores.
 #include "modem_tx_mfma.h"
+#include "modem_variants.h"
 
 namespace mk {
 
@@ -190,28 +191,6 @@ __global__ __launch_bounds__(256) void tx_fast(const TxParams p) {
     }
 }
 
-// Experiment switch (A/B builds only): MODEM_TX_WPE=4 asks for 4 waves per SIMD (<= 128 VGPRs)
-#ifdef MODEM_TX_WPE
-#define TX_WPE __attribute__((amdgpu_waves_per_eu(MODEM_TX_WPE)))
-#else
-#define TX_WPE
-#endif
-
-template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
-__global__ __launch_bounds__(256) TX_WPE void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
-    tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, blockIdx.x, gridDim.x);
-}
-
-// A batch of independent channels of one configuration (modem_tx_process_batch): workgroup
-// b serves channel b / g as its workgroup b % g of g.
-template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
-__global__ __launch_bounds__(256) TX_WPE void tx_mfma_batch(const TxBatch b, const th8* __restrict__ bfrag) {
-    const int ch = (int)(blockIdx.x / (unsigned)b.g);
-    const unsigned bid = blockIdx.x - (unsigned)ch * b.g;
-    const TxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
-    tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, bid, b.g);
-}
-
 // Any samples-per-symbol: thread per output sample, symbols staged in LDS.
 template <int OUT_MODE, typename OutT>
 __global__ __launch_bounds__(256) void tx_generic(const TxParams p) {
@@ -270,17 +249,50 @@ __device__ __forceinline__ float mod_trig_ieee(float x) {
 }
 
 // DMPSK / MFSK / BFSK: update() runs at every symbol tick (modulator.rs:90-93) with the
-// phase carried in f32 from symbol to symbol, so the states are a serial recurrence. One
-// workgroup: its lanes decode 256 symbol indices at a time into LDS, lane 0 runs the
-// recurrence exactly as the reference does, and the lanes write the states out.
+// phase carried in f32 from symbol to symbol, so the states are a serial recurrence (no exact
+// parallel form: the reachable f32 states do not close). One step, the reference's
+// f32 operations in its order:
 //   DMPSK (dmpsk.rs:29-33): phase = mod_trig(phase + sym * shift)
 //   MFSK (mfsk.rs:68-75):   off = mod_trig(off + (cur - next) * dev * s); cur = next
 //   BFSK (bfsk.rs:42-53):   on a change of bit, phase = mod_trig(phase + (b ? -dev*s : dev*(s-1)))
-// s is the carrier sample index after Carrier::next at the symbol's first sample.
-__global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
+// s (su) is the carrier sample index after Carrier::next at the symbol's first sample.
+struct ScanK {
+    int kind;
+    float shift, freq, max;
+    int map;
+    __device__ static ScanK of(const TxParams& p) { return ScanK{p.ph_kind, p.ph_shift, p.ph_freq, p.ph_max, p.ph_map}; }
+};
+template <int KIND>
+__device__ __forceinline__ float2 scan_step(const ScanK& k, float2 st, uint32_t idx, uint64_t su) {
 #pragma clang fp contract(off)
+    if (KIND == PH_DMPSK) {
+        st.x = mod_trig_ieee(st.x + (float)idx * k.shift);
+    } else if (KIND == PH_MFSK) {
+        const float next = k.map ? (float)(2 * (int)idx) : (float)(2 * (int)idx - (int)k.max);
+        st.y = st.y + (st.x - next) * k.freq * (float)su;
+        st.y = mod_trig_ieee(st.y);
+        st.x = next;
+    } else {                                   // BFSK: st = (phase, prev bit)
+        const float b = (float)(idx & 1u);
+        if (b != st.y) {
+            const float d = b == 1.0f ? -(k.freq * (float)su) : k.freq * (float)(su - 1u);
+            st.x = mod_trig_ieee(st.x + d);
+            st.y = b;
+        }
+    }
+    return st;
+}
+__device__ __forceinline__ float2 scan_step_any(const ScanK& k, float2 st, uint32_t idx, uint64_t su) {
+    return k.kind == PH_DMPSK ? scan_step<PH_DMPSK>(k, st, idx, su)
+         : k.kind == PH_MFSK  ? scan_step<PH_MFSK>(k, st, idx, su) : scan_step<PH_BFSK>(k, st, idx, su);
+}
+
+// One channel: its lanes decode 256 symbol indices at a time into LDS, lane 0 runs the
+// recurrence, and the lanes write the states out.
+__global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
     __shared__ uint32_t sidx[256];
     __shared__ float2 sst[256];
+    const ScanK k = ScanK::of(p);
     float2 st = p.hist[0];
     for (int64_t base = 0; base < p.nsym; base += 256) {
         const int64_t m = base + threadIdx.x;
@@ -289,23 +301,7 @@ __global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
         if (threadIdx.x == 0) {
             const int cnt = (int)(p.nsym - base < 256 ? p.nsym - base : 256);
             for (int j = 0; j < cnt; ++j) {
-                const uint32_t idx = sidx[j];
-                const uint64_t su = p.s0 + (uint64_t)(base + j) * (uint64_t)p.sps + 1u;
-                if (p.ph_kind == PH_DMPSK) {
-                    st.x = mod_trig_ieee(st.x + (float)idx * p.ph_shift);
-                } else if (p.ph_kind == PH_MFSK) {
-                    const float next = p.ph_map ? (float)(2 * (int)idx) : (float)(2 * (int)idx - (int)p.ph_max);
-                    st.y = st.y + (st.x - next) * p.ph_freq * (float)su;
-                    st.y = mod_trig_ieee(st.y);
-                    st.x = next;
-                } else {                                   // BFSK: st = (phase, prev bit)
-                    const float b = (float)(idx & 1u);
-                    if (b != st.y) {
-                        const float d = b == 1.0f ? -(p.ph_freq * (float)su) : p.ph_freq * (float)(su - 1u);
-                        st.x = mod_trig_ieee(st.x + d);
-                        st.y = b;
-                    }
-                }
+                st = scan_step_any(k, st, sidx[j], p.s0 + (uint64_t)(base + j) * (uint64_t)p.sps + 1u);
                 sst[j] = st;
             }
         }
@@ -314,6 +310,77 @@ __global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
         __syncthreads();
     }
     if (threadIdx.x == 0) p.hist_new[0] = st;
+}
+
+// A bank of channels of one scanned kind (modem_tx_process_batch): one lane per channel, each
+// running its own channel's recurrence with scan_step — the same operations in the same order
+// as tx_scan, so a channel's states are bit for bit those of its single call — 64 channels per
+// wave in lockstep. Each lane loads the next block of its symbol indices while it computes the
+// current block's states (the loads do not depend on the recurrence). ps: the channels'
+// parameter blocks in device memory (kernel arguments would hold only a few); each lane keeps
+// only the fields it uses in registers.
+template <int KIND>
+__global__ __launch_bounds__(64) void tx_scan_batch(const TxParams* __restrict__ ps, int nch) {
+    constexpr int B = 16;                      // symbols per block
+    const int c = (int)(blockIdx.x * 64 + threadIdx.x);
+    if (c >= nch) return;
+    const TxParams& q = ps[c];
+    const uint8_t* bits = q.bits;
+    const uint8_t* carry = q.carry;
+    const int ncarry = q.ncarry, bps = q.bps;
+    const bool fast = q.fast_bits != 0;
+    const int64_t nsym = q.nsym;
+    const uint64_t s0 = q.s0, sps = (uint64_t)q.sps;
+    float2* scan = q.scan;
+    const ScanK k = ScanK::of(q);
+    // bytes_to_bits (digital/util.rs:5-11) of symbol m, MSB first (tx_symbol_index's arithmetic)
+    auto index = [=](int64_t m) -> uint32_t {
+        uint32_t idx = 0;
+        if (fast) {                            // aligned words of 1, 2, 4 or 8 bytes
+            const uint8_t* b = bits + m * bps;
+            const uint64_t v = bps == 1 ? *b : bps == 2 ? *reinterpret_cast<const uint16_t*>(b)
+                             : bps == 4 ? *reinterpret_cast<const uint32_t*>(b) : *reinterpret_cast<const uint64_t*>(b);
+            return word_index(v, bps);
+        }
+        for (int j = 0; j < bps; ++j) {
+            const int64_t l = m * bps + j;
+            const uint8_t b = l < ncarry ? carry[l] : bits[l - ncarry];
+            idx = (idx << 1) | (b & 1u);
+        }
+        return idx;
+    };
+    uint32_t nxt[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) nxt[j] = j < nsym ? index(j) : 0u;
+    float2 st = q.hist[0];
+    for (int64_t m0 = 0; m0 < nsym; m0 += B) {
+        uint32_t cur[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) cur[j] = nxt[j];
+#pragma unroll
+        for (int j = 0; j < B; ++j) nxt[j] = m0 + B + j < nsym ? index(m0 + B + j) : 0u;
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            const int64_t m = m0 + j;
+            if (m < nsym) {
+                st = scan_step<KIND>(k, st, cur[j], s0 + (uint64_t)m * sps + 1u);
+                scan[m] = st;
+            }
+        }
+    }
+    q.hist_new[0] = st;
+}
+
+hipError_t launch_tx_scan_batch(const TxParams* dps, int nch, int kind, hipStream_t s) {
+    if (nch < 1) return hipSuccess;
+    const dim3 grid((unsigned)((nch + 63) / 64)), block(64);
+    switch (kind) {
+    case PH_DMPSK: hipLaunchKernelGGL(tx_scan_batch<PH_DMPSK>, grid, block, 0, s, dps, nch); break;
+    case PH_MFSK: hipLaunchKernelGGL(tx_scan_batch<PH_MFSK>, grid, block, 0, s, dps, nch); break;
+    case PH_BFSK: hipLaunchKernelGGL(tx_scan_batch<PH_BFSK>, grid, block, 0, s, dps, nch); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 __device__ __forceinline__ float2 tx_phasor_value(const TxParams& p, int64_t n, int64_t m) {
@@ -371,9 +438,9 @@ __global__ __launch_bounds__(256) void tx_phasor(const TxParams p) {
     }
 }
 
-hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s) {
+hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s, bool scanned) {
     const int64_t nsamp = p.nsym * p.sps;
-    if (p.scan != nullptr) {
+    if (p.scan != nullptr && !scanned) {
         hipLaunchKernelGGL(tx_scan, dim3(1), dim3(256), 0, s, p);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -419,78 +486,11 @@ static hipError_t tx_mode(const TxParams& p, int sps, int out_mode, hipStream_t 
 }
 
 
-template <int SPS, int NKS, int OM, typename OutT, int SUB>
-static hipError_t txm_go_sub(const TxParams& p, const void* bfrag, hipStream_t s) {
-    using K = TxMfma<SPS, NKS, OM, OutT, SUB>;
-    const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
-    const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << p.bps) * 8;
-    const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT, SUB>);
-    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT, SUB>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
-                       dim3(K::NT), lds, s, p, static_cast<const th8*>(bfrag));
-    return hipGetLastError();
-}
-template <int SPS, int NKS, int OM, typename OutT>
-static hipError_t txm_go(const TxParams& p, const void* bfrag, hipStream_t s) {
-    return tx_small_tiles(p.nsym, 16 / SPS) ? txm_go_sub<SPS, NKS, OM, OutT, 1>(p, bfrag, s)
-                                            : txm_go_sub<SPS, NKS, OM, OutT, 4>(p, bfrag, s);
-}
-template <int SPS, int NKS, int OM, typename OutT, int SUB>
-static hipError_t txm_go_batch_sub(TxBatch b, const void* bfrag, hipStream_t s) {
-    using K = TxMfma<SPS, NKS, OM, OutT, SUB>;
-    int64_t ntiles = 0;
-    for (int c = 0; c < b.nch; ++c) {
-        const int64_t t = (b.p[c].nsym + b.p[c].lead + K::TS - 1) / K::TS;
-        ntiles = t > ntiles ? t : ntiles;
-    }
-    const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << b.p[0].bps) * 8;
-    const void* k = reinterpret_cast<const void*>(&tx_mfma_batch<SPS, NKS, OM, OutT, SUB>);
-    const int64_t cap = persistent_grid(k, K::NT, lds, INT64_MAX);
-    int64_t g = cap / b.nch;
-    g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
-    b.g = (int32_t)g;
-    hipLaunchKernelGGL((tx_mfma_batch<SPS, NKS, OM, OutT, SUB>), dim3((unsigned)(g * b.nch)), dim3(K::NT), lds, s, b,
-                       static_cast<const th8*>(bfrag));
-    return hipGetLastError();
-}
-template <int SPS, int NKS, int OM, typename OutT>
-static hipError_t txm_go_batch(TxBatch b, const void* bfrag, hipStream_t s) {
-    int64_t nsym = 0;
-    for (int c = 0; c < b.nch; ++c) nsym += b.p[c].nsym;
-    return tx_small_tiles(nsym, 16 / SPS) ? txm_go_batch_sub<SPS, NKS, OM, OutT, 1>(b, bfrag, s)
-                                          : txm_go_batch_sub<SPS, NKS, OM, OutT, 4>(b, bfrag, s);
-}
-
-// (sps, k-steps) variants: W = 32 * nks >= 16/sps + K - 1 symbols (K = taps per phase).
-#ifdef MODEM_DEV_MIN      // experiment builds: the C2, C3 and C5 variants only
-#define TXM_TABLE(X) X(4, 1) X(4, 2) X(8, 3)    // C2, C3, C5
-#else
-#define TXM_TABLE(X) X(2, 1) X(2, 2) X(2, 3) X(2, 5) X(4, 1) X(4, 2) X(4, 3) X(4, 5) X(4, 9) \
-                     X(8, 1) X(8, 2) X(8, 3) X(8, 5) X(8, 9) X(16, 1) X(16, 2) X(16, 3) X(16, 5)
-#endif
-
-template <int OM, typename OutT>
-static hipError_t txm_sel(const TxParams& p, int sps, int nks, const void* bfrag, hipStream_t s) {
-#define TXM(S, N) if (sps == S && nks == N) return txm_go<S, N, OM, OutT>(p, bfrag, s);
-    TXM_TABLE(TXM)
-#undef TXM
-    return hipErrorInvalidValue;
-}
-
-template <typename OutT>
-static hipError_t txm_sel_batch(const TxBatch& b, int sps, int nks, const void* bfrag, hipStream_t s) {
-#define TXM(S, N) if (sps == S && nks == N) return txm_go_batch<S, N, OUT_IQ_MIXED, OutT>(b, bfrag, s);
-    TXM_TABLE(TXM)
-#undef TXM
-    return hipErrorInvalidValue;
-}
-
+// The matrix-core variants are instantiated in their own translation units (modem_txm_*.hip,
+// one per output form: the sources compile in parallel); here only their dispatch.
 hipError_t launch_tx_mfma_batch(const TxBatch& b, int sps, int nks, const void* bfrag, int dtype,
                                 hipStream_t s) {
     if (b.nch < 1 || b.nch > kBatchMax) return hipErrorInvalidValue;
-#ifdef MODEM_DEV_MIN
-    if (dtype != 0) return hipErrorInvalidValue;
-    return txm_sel_batch<float>(b, sps, nks, bfrag, s);
-#endif
     return dtype == 1 ? txm_sel_batch<__half>(b, sps, nks, bfrag, s) : txm_sel_batch<float>(b, sps, nks, bfrag, s);
 }
 
@@ -499,17 +499,13 @@ int tx_mfma_ksteps(int sps, int K) {
     const int need = (16 / sps + K - 1 + 31) / 32;
     int best = 0;
 #define TXK(S, N) if (sps == S && N >= need && (best == 0 || N < best)) best = N;
-    TXM_TABLE(TXK)
+    MODEM_TXM_TABLE(TXK)
 #undef TXK
     return best;
 }
 
 hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const void* bfrag, int dtype, int out_mode,
                           hipStream_t s) {
-#ifdef MODEM_DEV_MIN
-    if (dtype != 0 || out_mode != OUT_IQ_MIXED) return hipErrorInvalidValue;
-    return txm_sel<OUT_IQ_MIXED, float>(p, sps, nks, bfrag, s);
-#endif
     auto go = [&](auto outt) {
         using OutT = decltype(outt);
         switch (out_mode) {
@@ -522,9 +518,6 @@ hipError_t launch_tx_mfma(const TxParams& p, int sps, int nks, const void* bfrag
 }
 
 hipError_t launch_tx(const TxParams& p, int sps, int dtype, int out_mode, hipStream_t s) {
-#ifdef MODEM_DEV_MIN
-    return hipErrorInvalidValue;
-#endif
     return dtype == 1 ? tx_mode<__half>(p, sps, out_mode, s) : tx_mode<float>(p, sps, out_mode, s);
 }
 

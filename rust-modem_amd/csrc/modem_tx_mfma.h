@@ -85,18 +85,15 @@ __device__ __forceinline__ uint32_t word_index(uint64_t v, int bps) {
 // (lead = symbols before this call, mod SB), so a symbol always meets the same taps at the
 // same k positions and a stream cut into calls gives the same samples as one call.
 // Sample-and-hold (no taps) stays on the exact VALU kernels.
-#ifndef MODEM_TX_WIDE
-#define MODEM_TX_WIDE 1
-#endif
 template <int SPS, int SUB_> struct TxMfmaCfg {
     static constexpr int SB = 16 / SPS;          // symbols per row-block
     static constexpr int NT = 256;               // 4 waves
-    // 16x16 tiles per wave per tile: 4, 1 (small calls); at sps 8, 8 (round 5, MODEM_TX_WIDE):
+    // 16x16 tiles per wave per tile: 4, 1 (small calls); at sps 8, 8 (round 5):
     // 1024-symbol tiles like sps 4's, so the 94-symbol window halo is 8 % of the staged symbols
     // instead of 16 %, and a TX tile is exactly one RX tile (8192 samples), written on the XCD that
     // reads it back. C5 chain 259 -> 245.6 us (the RX in the chain 154.3 -> 142.8), C5 f16 175.2 ->
     // 169.2 us (profiles/r05_tx_wide.txt).
-    static constexpr int SUB = SUB_ == 4 && SPS == 8 && MODEM_TX_WIDE ? 8 : SUB_;
+    static constexpr int SUB = SUB_ == 4 && SPS == 8 ? 8 : SUB_;
     static constexpr int TS = 4 * SUB * 16 * SB; // symbols per workgroup tile
     static constexpr int NCOP = SB % 4 == 0 ? 1 : 4 / SB;   // plane copies (8-B aligned A reads)
 };
@@ -592,16 +589,11 @@ __device__ __forceinline__ void load_bfrag(const th8* __restrict__ bfrag, th8 (&
         bh[s] = bfrag[(2 * s) * 64 + lane];
         bl[s] = bfrag[(2 * s + 1) * 64 + lane];
     }
-#ifndef MODEM_TX_PIN_B          // experiment switch (A/B builds only)
-#define MODEM_TX_PIN_B 1
-#endif
-#if MODEM_TX_PIN_B
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
         asm volatile("" : "+v"(bh[s]));
         asm volatile("" : "+v"(bl[s]));
     }
-#endif
 }
 
 // One channel's share of a launch: workgroup `bid` of `nb` working on channel p.

@@ -47,7 +47,9 @@ CASES = [
     ("c3_qam16", 0, 5000, 3, 5, 1.0, None),         # small tiles, ragged, row-block lead cycles
     ("c3_qam16", 0, (1 << 18) + 4 * 37, 2, 3, 1.0, None),   # many small tiles, ragged
     ("c3_qam16", 0, 1 << 16, 0, 3, 1.0 / 64, 1),    # RX staged at a nonzero exponent
-    ("c5_qam256", 0, 7000, 5, 3, 1.0, None),        # 513 taps sps 8 (RX tile = two TX tiles), ragged
+    ("c5_qam256", 0, 7000, 5, 3, 1.0, None),        # 513 taps sps 8, ragged: at sps 8 the small
+                                                    # tiles give m = 2 (a 256-instant RX tile = 2048
+                                                    # samples = two 128-symbol TX tiles)
     ("c5_qam256", 0, 1 << 17, 0, 3, 1.0, 1),        # 513 taps sps 8, many tiles
     ("c5_qam256", 1, 1 << 17, 0, 3, 1.0, 1),        # f16 samples
     ("c2_qpsk", 1, 1 << 18, 1, 3, 1.0, None),       # f16 samples, ragged
