@@ -214,7 +214,11 @@ modem_status modem_tx_process(modem_tx* h, const uint8_t* bits, size_t nbits, vo
  * states as modem_tx_process(hs[c], bits[c], nbits[c], outs[c], caps[c], &produced[c], stream)
  * for c = 0 .. nch-1 in order. When every handle has the same matrix-core configuration
  * (sps, taps, bits per symbol, mixed I/Q output of one dtype, device) and every buffer is
- * device memory, up to 8 channels share one kernel launch; otherwise the calls run one by one.
+ * device memory, up to 8 channels share one kernel launch. When every handle has the same
+ * scanned phasor kind (DMPSK, MFSK, BFSK: a serial f32 state recurrence per stream,
+ * dmpsk.rs:29-33, mfsk.rs:68-75, bfsk.rs:42-53) and every buffer is device memory, the
+ * channels' state scans run as one launch, one lane per channel, each bit for bit its single
+ * call's. Otherwise the calls run one by one.
  * No reference counterpart (the reference drives one DigitalModulator per stream,
  * modulator.rs:64-101): the multi-channel form of that loop, SURVEY.md §8e. */
 modem_status modem_tx_process_batch(modem_tx* const* hs, size_t nch, const uint8_t* const* bits,
@@ -289,7 +293,9 @@ modem_status modem_chain_destroy(modem_chain* c);
  *   modem_tx_process(txs[i], bits[i], nbits[i], samples[i], caps[i], &n[i], stream);
  *   modem_rx_process(rxs[i], samples[i], n[i], out_iq[i], out_sym[i], out_caps[i], &k[i], stream);
  * run as one TX launch and then one RX launch per `group` consecutive channels (1 <= group <= 8;
- * a group's samples are re-read while they are still in the Infinity Cache). modem_chain_batch_create
+ * a group of at most 192 MiB of samples is re-read from the Infinity Cache, a larger one — C4's
+ * default 8 x 32 MiB — is stored non-temporally and re-read from HBM, which measured faster
+ * for it, profiles/r05_c4_policy.txt). modem_chain_batch_create
  * checks the buffers (device memory of the handles' one device) and the handles (one matrix-core
  * configuration for all TX and one for all RX handles, distinct handles, RX in_dtype = TX dtype,
  * complex mix, interleaved complex TX output) once: INVALID_ARG / UNSUPPORTED otherwise, nothing
@@ -297,7 +303,12 @@ modem_status modem_chain_destroy(modem_chain* c);
  * With more than one group the groups alternate between `stream` and a stream of the plan's
  * own (joined to `stream` by events at the start and end of every run), so that one group's RX
  * overlaps the next group's TX; the run is asynchronous on `stream` as a whole.
- * MODEM_CHAIN_BATCH_LANES=1 in the environment at create time keeps every launch on `stream`. */
+ * MODEM_CHAIN_BATCH_LANES=1 in the environment at create time keeps every launch on `stream`.
+ * Errors: CAPACITY (checked for every channel before any launch) leaves every handle untouched;
+ * a launch error (HIP) part-way through a run leaves the groups before it advanced and the
+ * rest not, so the plan is marked failed and every later run returns MODEM_ERR_HIP (destroy
+ * it; its handles' streams no longer line up). The caller's stream is still joined to the
+ * plan's own (best effort) so that it stays ordered after the launches already queued. */
 typedef struct modem_chain_batch modem_chain_batch;
 modem_status modem_chain_batch_create(modem_tx* const* txs, modem_rx* const* rxs, size_t nch, size_t group,
                                       const uint8_t* const* bits, const size_t* nbits, void* const* samples,

@@ -1035,7 +1035,9 @@ class ChainBatchPlan:
         self._fn = load_library().modem_chain_batch_run
 
     def run(self, stream=None):
-        """Returns (samples produced, kept instants produced) per channel."""
+        """Returns (samples produced, kept instants produced) per channel. A launch error part-way
+        through a run (ModemError, HIP) leaves some groups' handles advanced: the plan is then
+        failed in the library and every later run raises too."""
         _check(self._fn(self._h, self._prod, self._kout, _stream_handle(stream, self.txs[0].device)),
                "ChainBatchPlan.run")
         for tx, rx, k, n in zip(self.txs, self.rxs, self._nb, self._prod):

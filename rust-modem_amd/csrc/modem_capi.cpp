@@ -608,6 +608,7 @@ static void tx_fill(const modem_tx* h, const uint8_t* dbits, size_t nbits, bool 
     p.fast_bits = (h->ncarry == 0 && (h->bps == 1 || h->bps == 2 || h->bps == 4 || h->bps == 8) &&
                    ((uintptr_t)dbits % h->bps) == 0) ? 1 : 0;
     p.exact_idx = (h->sample + nsamp) <= (1ull << 53) ? 1 : 0;
+    p.idx46 = (h->sample + nsamp + 256) < (1ull << 46) ? 1 : 0;
     p.w = h->w;
     p.lut_h = h->d_luth;
     p.lut_scale_exp = h->lut_scale_exp;

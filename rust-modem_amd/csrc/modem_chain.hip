@@ -53,7 +53,7 @@ void chain_mfma(const TxParams tp, const th8* __restrict__ bfrag, const RxParams
         th8 bh[NKS_T], bl[NKS_T];
         load_bfrag(bfrag, bh, bl);
         bool done = false;
-        if (tp.fast_bits && tp.exact_idx && TK::out_ok(tp)) {
+        if (tp.fast_bits && tp.idx46 && TK::out_ok(tp)) {
             done = true;
             switch (tp.bps) {
             case 1: TK::template run<1>(tp, pl, lut_s, bh, bl, t0, t1, ts, xs); break;
@@ -125,7 +125,7 @@ void chain_small(const TxParams tp, const th8* __restrict__ bfrag, const RxParam
         th8 bh[NKS_T], bl[NKS_T];
         load_bfrag(bfrag, bh, bl);
         bool done = false;
-        if (tp.fast_bits && tp.exact_idx && TK::out_ok(tp)) {
+        if (tp.fast_bits && tp.idx46 && TK::out_ok(tp)) {
             done = true;
             switch (tp.bps) {
             case 1: TK::template one_tile<1>(tp, pl, pl2, lut_s, bh, bl, t, g.xs, ro); break;

@@ -38,6 +38,7 @@ struct TxParams {
     int32_t K;               // taps per polyphase branch = ceil(ntaps / sps)
     int32_t fast_bits;       // ncarry == 0, bps in {1,2,4,8}, bits aligned to bps bytes
     int32_t exact_idx;       // every carrier index of this call is < 2^53 (exact as f64)
+    int32_t idx46;           // ... and < 2^46 (tx_mfma's exact f32 index split, emit_full)
     float w;                 // Freq::sample_freq()
     // tx_mfma (split-f16 FIR): LUT as (re_hi, re_lo, im_hi, im_lo) halves of lut * 2^lut_scale_exp,
     // B fragments hold taps * 2^tap_scale_exp; lead = symbols before this call, mod 16/sps.

@@ -149,6 +149,13 @@ struct TxMfma {
     // made the tile loop's bits prefetch wait for itself at once (BPSK, QPSK).
     template <int BPS> using Word = typename std::conditional<BPS == 8, uint64_t, uint32_t>::type;
     template <int BPS>
+    __device__ static Word<BPS> load_word_rsrc(__amdgpu_buffer_rsrc_t r, int off) {
+        if constexpr (BPS == 1) return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+        else if constexpr (BPS == 2) return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0);
+        else if constexpr (BPS == 4) return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+        else return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    }
+    template <int BPS>
     __device__ static Word<BPS> load_word(const uint8_t* bits, int64_t m) {
         const uint8_t* b = bits + m * BPS;
         if (BPS == 1) return *b;
@@ -273,27 +280,36 @@ struct TxMfma {
         dim = m0;
     }
 
-    // Full 16x16 tile, carrier index < 2^53: unconditional stores. jt = call sample index of
-    // the sub-tile's first sample. Per sample: packed unscale (2^-kab), bit-exact phase,
-    // sin/cos, packed mix; stores through a uniform base + 32-bit lane offsets.
+    // Full 16x16 tile, carrier index < 2^46 (TxParams::idx46): unconditional stores. jt = call
+    // sample index of the sub-tile's first sample. Per sample: packed unscale (2^-kab), bit-exact
+    // phase, sin/cos, packed mix; stores through a uniform base + 32-bit lane offsets.
     template <bool RAW = false, bool NT = false>
     __device__ static void emit_full(const TxParams& p, int64_t jt, const f32x4& dre, const f32x4& dim, cf2 unscale,
                                      const RawOut& ro = RawOut{}) {
         const int lane = threadIdx.x & 63;
         int loff = 64 * (lane >> 4) + (lane & 15);          // sample of row r: loff + 16 r
         asm volatile("" : "+v"(loff));
-        const double nb = (double)(p.s0 + (uint64_t)jt) + (double)loff;
         cf2 z[4];
+        // the 2^-kab unscale always (exact; a multiply by 1 when kab = 0): as a uniform branch the
+        // compiler computed both sides and selected per register, 16 extra VALU per sub-tile
 #pragma unroll
-        for (int r = 0; r < 4; ++r) z[r] = (cf2){dre[r], dim[r]};
-        if (unscale.x != 1.0f) {                            // uniform; scale 1 is the usual case
-#pragma unroll
-            for (int r = 0; r < 4; ++r) z[r] *= unscale;
-        }
+        for (int r = 0; r < 4; ++r) z[r] = (cf2){dre[r], dim[r]} * unscale;
         if (OUT_MODE != OUT_IQ_BASEBAND) {
+            // `n as f32` of the sub-tile's samples n = n0 + loff + 16 r, n0 = s0 + jt (< 2^53 here):
+            // n0 = A + b with A a multiple of 2^sh exactly representable in f32 (sh from n0's top
+            // bit) and b < 2^23, so fl(A + (b + e)) — b + e an exact f32 integer — is the correctly
+            // rounded index (as RxMfma::idx_split): 2 packed adds per 4 samples instead of the f64
+            // index's 7 f64 operations and 4 conversions.
+            const uint64_t n0 = p.s0 + (uint64_t)jt;
+            const int eb = 63 - __builtin_clzll((n0 + 256) | 1);
+            const int sh = eb > 23 ? eb - 23 : 0;
+            const uint64_t A = n0 & ~((1ull << sh) - 1);
+            const float af = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                __builtin_bit_cast(uint32_t, __builtin_ldexpf((float)(uint32_t)(A >> sh), sh))));
+            const float bl = (float)((uint32_t)(n0 - A) + (uint32_t)loff);
             // rows (0, 1) and (2, 3) as two packed phase pairs, side by side
-            const cf2 nf0 = (cf2){idx_f32(nb), idx_f32(nb + 16.0)};
-            const cf2 nf1 = (cf2){idx_f32(nb + 32.0), idx_f32(nb + 48.0)};
+            const cf2 nf0 = ((cf2){bl, bl} + (cf2){0.f, 16.f}) + af;
+            const cf2 nf1 = ((cf2){bl, bl} + (cf2){32.f, 48.f}) + af;
             const cf2 ph0 = phase_from_f2(p.w, nf0), ph1 = phase_from_f2(p.w, nf1);
             cf2 sn0, cs0, sn1, cs1;
             sincos_phase2(ph0, sn0, cs0);
@@ -490,8 +506,9 @@ struct TxMfma {
         __syncthreads();                                            // the planes are restaged next
     }
 
-    // Tiles t0, t0 + ts, ... below t1 (xs > 0: first the last xs sub-tiles of tile t0 - 1). Tile t holds symbols [t*TS - lead, (t+1)*TS - lead) of the call. BPS > 0: bits aligned,
-    // no leftover bits, carrier index < 2^53 (the steady state); BPS == 0: general path only.
+    // Tiles t0, t0 + ts, ... below t1 (xs > 0: first the last xs sub-tiles of tile t0 - 1). Tile t
+    // holds symbols [t*TS - lead, (t+1)*TS - lead) of the call. BPS > 0: bits aligned, no leftover
+    // bits, carrier index < 2^46 (the steady state); BPS == 0: general path only.
     template <int BPS>
     __device__ __forceinline__ static void run(const TxParams& p, _Float16* pl, th4* lut_s, const th8 (&bh)[NKS],
                                const th8 (&bl)[NKS], int64_t t0, int64_t t1, int64_t ts, int xs = 0) {
@@ -501,21 +518,24 @@ struct TxMfma {
         const bool lv = p.levels != 0;
         const float us = __builtin_ldexpf(1.0f, -kab);             // exact (|kab| < 126)
         const cf2 unscale = {us, us};
-        const int64_t mlast = p.nsym_valid - 1;
         // full tile: every staged symbol is data of this call, every sample is emitted
         auto full = [&](int64_t t) {
             const int64_t ms = t * TS - lead - PRE;
             return BPS > 0 && ms >= 0 && ms + NE <= p.nsym_valid && t * TS - lead + TS <= p.nsym;
         };
         Word<BPS> pre[U];
+        // tile t's bits words through a buffer descriptor from its window's first symbol (a full
+        // tile's window lies inside the call; a prefetched tile that turns out not to be full is
+        // staged by stage_slow instead, so the zeros its out-of-range words read are never used):
+        // no per-slot 64-bit clamps (~35 VALU per tile and wave)
         auto prefetch = [&](int64_t t) {
             const int64_t ms = t * TS - lead - PRE;
+            const int64_t mb = ms < 0 ? 0 : ms;
+            const int64_t nrec = (p.nsym_valid - mb) * BPS;
+            const __amdgpu_buffer_rsrc_t rb = buf_rsrc(p.bits + mb * BPS,
+                                                       nrec <= 0 ? 0u : nrec > 0x7fffffff ? 0x7fffffffu : (uint32_t)nrec);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                int64_t m = ms + tid + NT * u;
-                m = m < 0 ? 0 : (m > mlast ? mlast : m);
-                pre[u] = load_word<BPS>(p.bits, m);
-            }
+            for (int u = 0; u < U; ++u) pre[u] = load_word_rsrc<BPS>(rb, (tid + NT * u) * BPS);
         };
         int64_t t = t0;
         // the first tile's bits are requested before the LUT goes to LDS, so that the two
@@ -612,7 +632,7 @@ __device__ __forceinline__ void tx_mfma_body(const TxParams& p, const th8* __res
     // (measured 1 % faster on C3 than contiguous ranges per workgroup)
     const int64_t t0 = bid, t1 = ntiles, ts = nb;
     if (t0 >= t1) return;
-    if (p.fast_bits && p.exact_idx && K::out_ok(p)) {   // one uniform switch: the tile loop is specialised
+    if (p.fast_bits && p.idx46 && K::out_ok(p)) {      // one uniform switch: the tile loop is specialised
         switch (p.bps) {
         case 1: K::template run<1>(p, pl, lut_s, bh, bl, t0, t1, ts); return;
         case 2: K::template run<2>(p, pl, lut_s, bh, bl, t0, t1, ts); return;

@@ -277,3 +277,32 @@ def test_tx_f16_output_only_4_byte_aligned(m, o, torch_cuda):
     got = tx().process(bits, out=out)
     assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
     assert torch.equal(big[0], torch.zeros(2, dtype=torch.float16, device="cuda"))
+
+
+@pytest.mark.parametrize("nsamp,cuts", [
+    (1 << 19, [4096 * 4 - 1, 4096 * 4 + 1, 17, 4 * 1024 * 16 - 4, 65537, 2, 4 * 1024 * 9 + 61, 131071]),
+    ((1 << 23) + 4 * 1024 * 5 + 6, [(1 << 22) + 4 * 37 + 3]),
+])
+def test_rx_f16_chunk_tails(m, o, torch_cuda, nsamp, cuts):
+    """f16 samples in and out: calls whose last tile is partial at odd offsets, bitwise equal to one
+    call, on the small tiles (2^19 samples) and on the 1024-instant tiles (calls of >= 2^22
+    samples). The fast path stores f16 I/Q two instants per lane (whole 128-B lines): a pair
+    straddling a call's last instant must still write its first (per-dword range check)."""
+    torch = torch_cuda
+    name, bps, L, sps = CONFIGS["c3_qam16"]
+    bits = torch.from_numpy(o.prng_bits(SEED + 21, nsamp // sps * bps)).cuda()
+    taps = m.rrc_taps(L, sps, 0.35)
+    w = o.sample_freq(1, 4)
+    x = m.DigitalModulator(m.Carrier(w), product_phasor(m, name), sps, taps, dtype=1).process(bits)
+
+    def rx():
+        return m.DemodulatorRx(m.Carrier(w), taps, decim=sps, decim_offset=L - 1, mix=m.MIX_COMPLEX,
+                               slicer=product_phasor(m, name).slicer(), in_dtype=1, out_dtype=1)
+    iq1, s1 = rx().process(x)
+    r = rx()
+    iqs, ss, pos = [], [], 0
+    for c in cuts + [x.shape[0] - sum(cuts)]:
+        i_, s_ = r.process(x[pos:pos + c])
+        iqs.append(host(i_)); ss.append(host(s_)); pos += c
+    assert np.array_equal(np.concatenate(iqs).view(np.uint16), host(iq1).view(np.uint16))
+    assert np.array_equal(np.concatenate(ss), host(s1))

@@ -27,11 +27,11 @@ for rep in $(seq 1 ${REPS:-2}); do
       path=""; [ "$lib" != tree ] && path="$PWD/rust-modem_amd/build/var/$lib/libmodem_hip.so"
       tag=$(echo "${cfg}_$v" | tr ':=,' '___')
       env $envs RUST_MODEM_AMD_LIB=$path timeout -k 10 300 python3 bench.py --config $cfg $B > $o/$tag.json 2> $o/$tag.err || { tail -3 $o/$tag.err; exit 1; }
-      line $o/$tag.json "$cfg $v"
+      line $o/$tag.json "$cfg $v" | tee -a $o/lines.txt
     done
   done
 done
 for i in $(seq 1 ${DRV:-0}); do
   timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $o/c3_drv$i.json 2> $o/c3_drv$i.err || { tail -3 $o/c3_drv$i.err; exit 1; }
-  line $o/c3_drv$i.json "c3 driver-style $i"
+  line $o/c3_drv$i.json "c3 driver-style $i" | tee -a $o/lines.txt
 done
