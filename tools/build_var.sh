@@ -11,7 +11,7 @@ d=build/var/$name; mkdir -p $d
 MIN=-DMODEM_VARIANTS_MIN; [ "${FULL:-0}" = 1 ] && MIN=
 srcs="tx rx chain misc txm_f32 txm_f16 txm_bb txm_real rxm_f32 rxm_f16 rxm_mixed"
 for f in $srcs; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize --offload-arch=gfx950 $MIN "$@" \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form=1 --offload-arch=gfx950 $MIN "$@" \
     -c csrc/modem_$f.hip -o $d/$f.o &
 done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $MIN "$@" -x hip -c csrc/modem_capi.cpp -o $d/c.o &
