@@ -241,11 +241,20 @@ static hipError_t tx_go(const TxParams& p, hipStream_t s) {
 // Rust's `as f32`; f32 operations in the reference's left-to-right order.
 enum { PH_DCQPSK = 8, PH_DMPSK = 9, PH_CPFSK = 10, PH_MSK = 11, PH_MFSK = 12, PH_BFSK = 13 };
 
-// mod_trig (util.rs:3-6) with the IEEE quotient, for any finite f32 (the scan's phases can be
-// negative, where the carrier's shortcut is not proven).
+// mod_trig (util.rs:3-6: x - TWO_PI * floor(x / TWO_PI), the quotient an IEEE f32 division) for
+// any f32 (the scan's phases can be negative), without the division: the carrier's division-free
+// floor (phase_from_f: q0 = x RC, r = fma(-q0, TWO_PI, x), q1 = fma(r, RC, q0)) gives the same
+// result bit for bit for every finite f32 once -0 is mapped to +0 (x + 0: the identity elsewhere;
+// the reference gives +0 for -0, the division-free form -0). tools/mod_trig_check.cpp checks all
+// 2^32 inputs: 0 mismatches. The IEEE division was ~11 dependent instructions of the scans' serial
+// step (profiles/r06_scan_rate.txt).
 __device__ __forceinline__ float mod_trig_ieee(float x) {
 #pragma clang fp contract(off)
-    return x - kTwoPi * __builtin_floorf(x / kTwoPi);
+    const float xz = x + 0.0f;
+    const float q0 = xz * kRcp2Pi;
+    const float r = __builtin_fmaf(-q0, kTwoPi, xz);
+    const float q1 = __builtin_fmaf(r, kRcp2Pi, q0);
+    return xz - kTwoPi * __builtin_floorf(q1);
 }
 
 // DMPSK / MFSK / BFSK: update() runs at every symbol tick (modulator.rs:90-93) with the
@@ -312,68 +321,88 @@ __global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
     if (threadIdx.x == 0) p.hist_new[0] = st;
 }
 
-// A bank of channels of one scanned kind (modem_tx_process_batch): one lane per channel, each
-// running its own channel's recurrence with scan_step — the same operations in the same order
-// as tx_scan, so a channel's states are bit for bit those of its single call — 64 channels per
-// wave in lockstep. Each lane loads the next block of its symbol indices while it computes the
-// current block's states (the loads do not depend on the recurrence). ps: the channels'
-// parameter blocks in device memory (kernel arguments would hold only a few); each lane keeps
-// only the fields it uses in registers.
+// A bank of channels of one scanned kind (modem_tx_process_batch): one lane of wave 0 per channel
+// (64 channels per workgroup) runs that channel's recurrence with scan_step — the same operations in
+// the same order as tx_scan, so a channel's states are bit for bit those of its single call — while
+// waves 1-3 stream the symbols through LDS: they decode block b + 1's symbol indices (each wave
+// instruction one channel's 64 consecutive symbols, coalesced) and write block b - 1's states out,
+// both double-buffered, one barrier per block. (The first form, one lane per channel loading its own
+// symbols and storing its own states, touched 64 lines per memory instruction: 3 Msymbols/s per
+// lane, profiles/r06_scan_rate.txt.) ps: the channels' parameter blocks in device memory.
 template <int KIND>
-__global__ __launch_bounds__(64) void tx_scan_batch(const TxParams* __restrict__ ps, int nch) {
-    constexpr int B = 16;                      // symbols per block
-    const int c = (int)(blockIdx.x * 64 + threadIdx.x);
-    if (c >= nch) return;
-    const TxParams& q = ps[c];
-    const uint8_t* bits = q.bits;
-    const uint8_t* carry = q.carry;
-    const int ncarry = q.ncarry, bps = q.bps;
-    const bool fast = q.fast_bits != 0;
-    const int64_t nsym = q.nsym;
-    const uint64_t s0 = q.s0, sps = (uint64_t)q.sps;
-    float2* scan = q.scan;
-    const ScanK k = ScanK::of(q);
-    // bytes_to_bits (digital/util.rs:5-11) of symbol m, MSB first (tx_symbol_index's arithmetic)
-    auto index = [=](int64_t m) -> uint32_t {
-        uint32_t idx = 0;
-        if (fast) {                            // aligned words of 1, 2, 4 or 8 bytes
-            const uint8_t* b = bits + m * bps;
-            const uint64_t v = bps == 1 ? *b : bps == 2 ? *reinterpret_cast<const uint16_t*>(b)
-                             : bps == 4 ? *reinterpret_cast<const uint32_t*>(b) : *reinterpret_cast<const uint64_t*>(b);
-            return word_index(v, bps);
+__global__ __launch_bounds__(256) void tx_scan_batch(const TxParams* __restrict__ ps, int nch) {
+    constexpr int B = 64, S = B + 1;           // symbols per block; LDS row stride (conflict-free columns)
+    __shared__ uint32_t sidx[2][64 * S];
+    __shared__ float2 sst[2][64 * S];
+    const int c0 = (int)blockIdx.x * 64;
+    const int nc = nch - c0 < 64 ? nch - c0 : 64;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
+    int64_t nmax = 0;
+    for (int c = 0; c < nc; ++c) nmax = ps[c0 + c].nsym > nmax ? ps[c0 + c].nsym : nmax;
+    const int64_t nblk = (nmax + B - 1) / B;
+    // waves 1-3: channel rows c = wave - 1, wave + 2, ... of block blk (issuing every row's loads
+    // before the LDS writes measured no faster: 12.1 vs 11.2 ms for 64 x 2^16 DMPSK symbols)
+    auto load_block = [&](int64_t blk) {
+        for (int c = wave - 1; c < nc; c += 3) {
+            const TxParams& q = ps[c0 + c];
+            const int64_t m = blk * B + lane;
+            sidx[blk & 1][c * S + lane] = m < q.nsym ? tx_symbol_index(q, m) : 0u;
         }
-        for (int j = 0; j < bps; ++j) {
-            const int64_t l = m * bps + j;
-            const uint8_t b = l < ncarry ? carry[l] : bits[l - ncarry];
-            idx = (idx << 1) | (b & 1u);
-        }
-        return idx;
     };
-    uint32_t nxt[B];
-#pragma unroll
-    for (int j = 0; j < B; ++j) nxt[j] = j < nsym ? index(j) : 0u;
-    float2 st = q.hist[0];
-    for (int64_t m0 = 0; m0 < nsym; m0 += B) {
-        uint32_t cur[B];
-#pragma unroll
-        for (int j = 0; j < B; ++j) cur[j] = nxt[j];
-#pragma unroll
-        for (int j = 0; j < B; ++j) nxt[j] = m0 + B + j < nsym ? index(m0 + B + j) : 0u;
-#pragma unroll
-        for (int j = 0; j < B; ++j) {
-            const int64_t m = m0 + j;
-            if (m < nsym) {
-                st = scan_step<KIND>(k, st, cur[j], s0 + (uint64_t)m * sps + 1u);
-                scan[m] = st;
-            }
+    auto store_block = [&](int64_t blk) {
+        for (int c = wave - 1; c < nc; c += 3) {
+            const TxParams& q = ps[c0 + c];
+            const int64_t m = blk * B + lane;
+            if (m < q.nsym) q.scan[m] = sst[blk & 1][c * S + lane];
         }
+    };
+    float2 st = make_float2(0.f, 0.f);
+    ScanK k{};
+    int64_t nsym = 0;
+    uint64_t s0 = 0, sps = 0;
+    if (wave == 0 && lane < nc) {
+        const TxParams& q = ps[c0 + lane];
+        st = q.hist[0];
+        k = ScanK::of(q);
+        nsym = q.nsym;
+        s0 = q.s0;
+        sps = (uint64_t)q.sps;
     }
-    q.hist_new[0] = st;
+    if (wave > 0) load_block(0);
+    __syncthreads();
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+        if (wave == 0) {
+            if (lane < nc) {
+                const uint32_t* ix = &sidx[blk & 1][lane * S];
+                float2* so = &sst[blk & 1][lane * S];
+                const int64_t mb = blk * B;
+                const int cnt = nsym - mb < B ? (int)(nsym - mb) : B;   // (<= 0: this channel is done)
+                for (int j0 = 0; j0 < cnt; j0 += 16) {
+                    uint32_t v[16];                    // the next 16 indices read ahead of the steps
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) v[i] = ix[j0 + i];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        if (j0 + i < cnt) {
+                            st = scan_step<KIND>(k, st, v[i], s0 + (uint64_t)(mb + j0 + i) * sps + 1u);
+                            so[j0 + i] = st;
+                        }
+                    }
+                }
+            }
+        } else {
+            if (blk + 1 < nblk) load_block(blk + 1);
+            if (blk > 0) store_block(blk - 1);
+        }
+        __syncthreads();
+    }
+    if (wave > 0 && nblk > 0) store_block(nblk - 1);
+    if (wave == 0 && lane < nc) ps[c0 + lane].hist_new[0] = st;
 }
 
 hipError_t launch_tx_scan_batch(const TxParams* dps, int nch, int kind, hipStream_t s) {
     if (nch < 1) return hipSuccess;
-    const dim3 grid((unsigned)((nch + 63) / 64)), block(64);
+    const dim3 grid((unsigned)((nch + 63) / 64)), block(256);
     switch (kind) {
     case PH_DMPSK: hipLaunchKernelGGL(tx_scan_batch<PH_DMPSK>, grid, block, 0, s, dps, nch); break;
     case PH_MFSK: hipLaunchKernelGGL(tx_scan_batch<PH_MFSK>, grid, block, 0, s, dps, nch); break;
