@@ -241,6 +241,32 @@ static inline unsigned persistent_grid(const void* kernel, int threads, size_t l
 }
 
 
+// XCD-chunked tile slots of a persistent grid (tx_mfma / rx_mfma): workgroups are dealt to the 8
+// XCDs round-robin (block b on XCD b mod 8), and a grid-strided walk (tile slot + k nb) puts
+// neighbouring tiles on different XCDs, so a tile's window halo (the bits before a TX tile, the
+// samples before an RX tile) is read from another XCD's L2 or from HBM. Block 8 j + x takes slot
+// (8 (j / c) + x) c + j mod c instead: runs of c consecutive tiles per XCD, the slot still a
+// bijection on [0, nb) when 8 c divides nb (xcd_chunk), every XCD's tiles advancing by nb per
+// round, and tile i on XCD (i / c) mod 8 for any such grid, so the TX and the RX still meet on
+// the XCD that wrote a tile. c = 1 is the plain walk.
+__device__ __forceinline__ int64_t xcd_slot(int64_t bid, int c) {
+    if (c <= 1) return bid;
+    const int64_t j = bid >> 3, x = bid & 7;
+    return ((j / c) * 8 + x) * c + j % c;
+}
+// the chunk for a grid of nb workgroups: MODEM_XCD_CHUNK (default 8) halved until 8 c divides nb
+static inline int xcd_chunk(int64_t nb) {
+    static const int c0 = [] {
+        const char* e = std::getenv("MODEM_XCD_CHUNK");
+        const int v = e ? std::atoi(e) : 8;
+        return v >= 1 ? v : 1;
+    }();
+    int c = c0;
+    while (c > 1 && nb % (8 * (int64_t)c) != 0) c >>= 1;
+    return c;
+}
+
+
 // acc_re/acc_im += sum_s A_s * B_s over NKS k-steps; A_s (complex) is read from LDS at
 // arow[off(s)], PD k-steps ahead of its MFMA pair (explicit software pipeline: the
 // scheduling barriers keep the compiler from collapsing it to one read of look-ahead).

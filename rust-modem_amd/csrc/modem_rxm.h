@@ -11,8 +11,8 @@ namespace mk {
 
 template <int DEC, int NKS, typename InT, int MIX, typename OutT, int NWF, int EM, int KS>
 __global__ __launch_bounds__(256 * KS) __attribute__((amdgpu_waves_per_eu(RxMfma<DEC, NKS, InT, MIX, OutT, NWF, KS>::WPE)))
-void rx_mfma(const RxParams p, const _Float16* __restrict__ tables) {
-    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>(p, tables, blockIdx.x, gridDim.x);
+void rx_mfma(const RxParams p, const _Float16* __restrict__ tables, int xc) {
+    rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>(p, tables, xcd_slot(blockIdx.x, xc), gridDim.x);
 }
 
 // A batch of independent channels of one configuration (modem_rx_process_batch): workgroup
@@ -35,8 +35,9 @@ static hipError_t rxm_go_em(const RxParams& p, const void* tables, hipStream_t s
     using K = RxMfma<DEC, NKS, InT, MIX, OutT, NWF, KS>;
     const int64_t ntiles = (p.nout + (p.k_first & 15) + K::TS - 1) / K::TS;
     const void* k = reinterpret_cast<const void*>(&rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>);
-    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>), dim3(persistent_grid(k, K::NT, K::LDS_BYTES, ntiles)),
-                       dim3(K::NT), K::LDS_BYTES, s, p, static_cast<const _Float16*>(tables));
+    const unsigned grid = persistent_grid(k, K::NT, K::LDS_BYTES, ntiles);
+    hipLaunchKernelGGL((rx_mfma<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>), dim3(grid), dim3(K::NT), K::LDS_BYTES, s, p,
+                       static_cast<const _Float16*>(tables), xcd_chunk(grid));
     return hipGetLastError();
 }
 

@@ -9,8 +9,8 @@
 namespace mk {
 
 template <int SPS, int NKS, int OUT_MODE, typename OutT, int SUB>
-__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __restrict__ bfrag) {
-    tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, blockIdx.x, gridDim.x);
+__global__ __launch_bounds__(256) void tx_mfma(const TxParams p, const th8* __restrict__ bfrag, int xc) {
+    tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, xcd_slot(blockIdx.x, xc), gridDim.x);
 }
 
 // A batch of independent channels of one configuration (modem_tx_process_batch): workgroup
@@ -33,8 +33,9 @@ static hipError_t txm_go_sub(const TxParams& p, const void* bfrag, hipStream_t s
     const int64_t ntiles = (p.nsym + p.lead + K::TS - 1) / K::TS;
     const size_t lds = (size_t)K::PLANES * 2 + ((size_t)1 << p.bps) * 8;
     const void* k = reinterpret_cast<const void*>(&tx_mfma<SPS, NKS, OM, OutT, SUB>);
-    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT, SUB>), dim3(persistent_grid(k, K::NT, lds, ntiles)),
-                       dim3(K::NT), lds, s, p, static_cast<const th8*>(bfrag));
+    const unsigned grid = persistent_grid(k, K::NT, lds, ntiles);
+    hipLaunchKernelGGL((tx_mfma<SPS, NKS, OM, OutT, SUB>), dim3(grid), dim3(K::NT), lds, s, p,
+                       static_cast<const th8*>(bfrag), xcd_chunk(grid));
     return hipGetLastError();
 }
 template <int SPS, int NKS, int OM, typename OutT>

@@ -22,14 +22,14 @@ LIB = os.path.join(ROOT, "rust-modem_amd", "lib", "libmodem_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 
 KERNELS = {
-    "c3 rx": "_ZN2mk7rx_mfmaILi4ELi6EfLi0EfLi4ELi3ELi1EEEvNS_8RxParamsEPKDF16_",
-    "c3 tx": "_ZN2mk7tx_mfmaILi4ELi2ELi0EfLi4EEEvNS_8TxParamsEPKDv8_DF16_",
+    "c3 rx": "_ZN2mk7rx_mfmaILi4ELi6EfLi0EfLi4ELi3ELi1EEEvNS_8RxParamsEPKDF16_i",
+    "c3 tx": "_ZN2mk7tx_mfmaILi4ELi2ELi0EfLi4EEEvNS_8TxParamsEPKDv8_DF16_i",
     "c4 rx batch": "_ZN2mk13rx_mfma_batchILi4ELi4EfLi0EfLi4ELi7ELi1EEEvNS_7RxBatchEPKDF16_",
     "c4 tx batch": "_ZN2mk13tx_mfma_batchILi4ELi1ELi0EfLi4EEEvNS_7TxBatchEPKDv8_DF16_",
-    "c5 rx (k-split)": "_ZN2mk7rx_mfmaILi8ELi20EfLi0EfLi4ELi3ELi2EEEvNS_8RxParamsEPKDF16_",
-    "c5 tx": "_ZN2mk7tx_mfmaILi8ELi3ELi0EfLi4EEEvNS_8TxParamsEPKDv8_DF16_",
-    "c5 f16 rx": "_ZN2mk7rx_mfmaILi8ELi20E6__halfLi0ES1_Li4ELi3ELi1EEEvNS_8RxParamsEPKDF16_",
-    "c5 f16 tx": "_ZN2mk7tx_mfmaILi8ELi3ELi0E6__halfLi4EEEvNS_8TxParamsEPKDv8_DF16_",
+    "c5 rx (k-split)": "_ZN2mk7rx_mfmaILi8ELi20EfLi0EfLi4ELi3ELi2EEEvNS_8RxParamsEPKDF16_i",
+    "c5 tx": "_ZN2mk7tx_mfmaILi8ELi3ELi0EfLi4EEEvNS_8TxParamsEPKDv8_DF16_i",
+    "c5 f16 rx": "_ZN2mk7rx_mfmaILi8ELi20E6__halfLi0ES1_Li4ELi3ELi1EEEvNS_8RxParamsEPKDF16_i",
+    "c5 f16 tx": "_ZN2mk7tx_mfmaILi8ELi3ELi0E6__halfLi4EEEvNS_8TxParamsEPKDv8_DF16_i",
 }
 
 
