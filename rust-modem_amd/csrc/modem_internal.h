@@ -130,10 +130,10 @@ hipError_t launch_tx_scan_batch(const TxParams* dps, int nch, int kind, hipStrea
 int tx_mfma_ksteps(int sps, int K);
 // Channel batches (modem_tx_process_batch / modem_rx_process_batch): up to kBatchMax
 // independent handles of one configuration in one launch; the launcher sets g, the
-// workgroups per channel (workgroup b serves channel b / g).
+// workgroups per channel (workgroup b serves channel b / g), rot and xc (xcd_chunk of g).
 constexpr int kBatchMax = 8;
-struct TxBatch { TxParams p[kBatchMax]; int32_t nch; int32_t g; int32_t rot; };
-struct RxBatch { RxParams p[kBatchMax]; int32_t nch; int32_t g; int32_t rot; };
+struct TxBatch { TxParams p[kBatchMax]; int32_t nch; int32_t g; int32_t rot; int32_t xc; };
+struct RxBatch { RxParams p[kBatchMax]; int32_t nch; int32_t g; int32_t rot; int32_t xc; };
 // The per-channel rotation of a batch launch's workgroups (a multiple of 8, so that every tile
 // keeps its XCD slot: blocks b and b + 8 share an XCD); 0 when g is not a multiple of 8.
 // MODEM_BATCH_ROT=0 in the environment turns it off (A/B).

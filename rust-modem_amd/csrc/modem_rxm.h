@@ -26,6 +26,7 @@ void rx_mfma_batch(const RxBatch b, const _Float16* __restrict__ tables) {
     // other channels' workgroup 0
     unsigned bid = blockIdx.x - (unsigned)ch * b.g + (unsigned)(ch * b.rot);
     bid = bid >= (unsigned)b.g ? bid - (unsigned)b.g : bid;
+    bid = (unsigned)xcd_slot(bid, b.xc);    // the channel's XCD-chunked slot (b.g a multiple of 8 b.xc)
     const RxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
     rx_mfma_body<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>(p, tables, bid, b.g);
 }
@@ -55,6 +56,7 @@ static hipError_t rxm_go_batch_em(RxBatch b, const void* tables, hipStream_t s) 
     g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
     b.g = (int32_t)g;
     b.rot = batch_rot(b.g, b.nch);
+    b.xc = xcd_chunk(b.g);
     hipLaunchKernelGGL((rx_mfma_batch<DEC, NKS, InT, MIX, OutT, NWF, EM, KS>), dim3((unsigned)(g * b.nch)),
                        dim3(K::NT), K::LDS_BYTES, s, b, static_cast<const _Float16*>(tables));
     return hipGetLastError();

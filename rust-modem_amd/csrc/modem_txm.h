@@ -23,6 +23,7 @@ __global__ __launch_bounds__(256) void tx_mfma_batch(const TxBatch b, const th8*
     // other channels' workgroup 0
     unsigned bid = blockIdx.x - (unsigned)ch * b.g + (unsigned)(ch * b.rot);
     bid = bid >= (unsigned)b.g ? bid - (unsigned)b.g : bid;
+    bid = (unsigned)xcd_slot(bid, b.xc);    // the channel's XCD-chunked slot (b.g a multiple of 8 b.xc)
     const TxParams p = b.p[ch];     // one bulk copy: the body's uses read registers, not kernarg
     tx_mfma_body<SPS, NKS, OUT_MODE, OutT, SUB>(p, bfrag, bid, b.g);
 }
@@ -58,6 +59,7 @@ static hipError_t txm_go_batch_sub(TxBatch b, const void* bfrag, hipStream_t s) 
     g = g < 1 ? 1 : g > ntiles ? (ntiles > 0 ? ntiles : 1) : g;
     b.g = (int32_t)g;
     b.rot = batch_rot(b.g, b.nch);
+    b.xc = xcd_chunk(b.g);
     hipLaunchKernelGGL((tx_mfma_batch<SPS, NKS, OM, OutT, SUB>), dim3((unsigned)(g * b.nch)), dim3(K::NT), lds, s, b,
                        static_cast<const th8*>(bfrag));
     return hipGetLastError();
