@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """C2's fused launch (chain_small) by phase, from per-workgroup s_memrealtime stamps (100 MHz) of a
-probe build (-DMODEM_PROBE_STAMPS: tools/build_var.sh stamps -DMODEM_PROBE_STAMPS; the library is
-taken from RUST_MODEM_AMD_LIB). Stamps per workgroup (thread 0): 0 entry, 1 the TX part done (its
+probe build: round 6 built it with a temporary MODEM_PROBE_STAMPS switch in modem_chain.hip (a
+__device__ g_stamps[4096 * 16] array, thread 0 storing the stamps and each wave's HW_ID / XCC_ID at
+slots 0-4, 5 and 8-11, and an exported modem_probe_stamps(out, n) copying it back), removed after the
+measurement (profiles/r06_c2_stamps.txt); the library is taken from RUST_MODEM_AMD_LIB. Stamps per workgroup (thread 0): 0 entry, 1 the TX part done (its
 stores issued), 2 the RX tap tables in LDS, 3 the RX part done (its stores issued), 4 every store
 acknowledged. For isolated launches (step; synchronize) and the last of a back-to-back run, the
 percentiles over the 1024 workgroups of each phase and of the entry skew, in us.
