@@ -322,20 +322,24 @@ __global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
 }
 
 // A bank of channels of one scanned kind (modem_tx_process_batch): one lane of wave 0 per channel
-// (64 channels per workgroup) runs that channel's recurrence with scan_step — the same operations in
+// (kScanCpw channels per workgroup) runs that channel's recurrence with scan_step — the same operations in
 // the same order as tx_scan, so a channel's states are bit for bit those of its single call — while
 // waves 1-3 stream the symbols through LDS: they decode block b + 1's symbol indices (each wave
 // instruction one channel's 64 consecutive symbols, coalesced) and write block b - 1's states out,
 // both double-buffered, one barrier per block. (The first form, one lane per channel loading its own
 // symbols and storing its own states, touched 64 lines per memory instruction: 3 Msymbols/s per
-// lane, profiles/r06_scan_rate.txt.) ps: the channels' parameter blocks in device memory.
+// lane, profiles/r06_scan_rate.txt.) 16 channels per workgroup rather than 64: the three streaming
+// waves, not the recurrences, bounded a 64-channel workgroup (a bank of 64 DMPSK channels 352 ->
+// 1090 Msymbols/s, MFSK 351 -> 682, BFSK 400 -> 490; 8 per workgroup measured the same as 16).
+// ps: the channels' parameter blocks in device memory.
+constexpr int kScanCpw = 16;
 template <int KIND>
 __global__ __launch_bounds__(256) void tx_scan_batch(const TxParams* __restrict__ ps, int nch) {
     constexpr int B = 64, S = B + 1;           // symbols per block; LDS row stride (conflict-free columns)
-    __shared__ uint32_t sidx[2][64 * S];
-    __shared__ float2 sst[2][64 * S];
-    const int c0 = (int)blockIdx.x * 64;
-    const int nc = nch - c0 < 64 ? nch - c0 : 64;
+    __shared__ uint32_t sidx[2][kScanCpw * S];
+    __shared__ float2 sst[2][kScanCpw * S];
+    const int c0 = (int)blockIdx.x * kScanCpw;
+    const int nc = nch - c0 < kScanCpw ? nch - c0 : kScanCpw;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     int64_t nmax = 0;
     for (int c = 0; c < nc; ++c) nmax = ps[c0 + c].nsym > nmax ? ps[c0 + c].nsym : nmax;
@@ -402,7 +406,7 @@ __global__ __launch_bounds__(256) void tx_scan_batch(const TxParams* __restrict_
 
 hipError_t launch_tx_scan_batch(const TxParams* dps, int nch, int kind, hipStream_t s) {
     if (nch < 1) return hipSuccess;
-    const dim3 grid((unsigned)((nch + 63) / 64)), block(256);
+    const dim3 grid((unsigned)((nch + kScanCpw - 1) / kScanCpw)), block(256);
     switch (kind) {
     case PH_DMPSK: hipLaunchKernelGGL(tx_scan_batch<PH_DMPSK>, grid, block, 0, s, dps, nch); break;
     case PH_MFSK: hipLaunchKernelGGL(tx_scan_batch<PH_MFSK>, grid, block, 0, s, dps, nch); break;
