@@ -291,35 +291,7 @@ __device__ __forceinline__ float2 scan_step(const ScanK& k, float2 st, uint32_t 
     }
     return st;
 }
-__device__ __forceinline__ float2 scan_step_any(const ScanK& k, float2 st, uint32_t idx, uint64_t su) {
-    return k.kind == PH_DMPSK ? scan_step<PH_DMPSK>(k, st, idx, su)
-         : k.kind == PH_MFSK  ? scan_step<PH_MFSK>(k, st, idx, su) : scan_step<PH_BFSK>(k, st, idx, su);
-}
 
-// One channel: its lanes decode 256 symbol indices at a time into LDS, lane 0 runs the
-// recurrence, and the lanes write the states out.
-__global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
-    __shared__ uint32_t sidx[256];
-    __shared__ float2 sst[256];
-    const ScanK k = ScanK::of(p);
-    float2 st = p.hist[0];
-    for (int64_t base = 0; base < p.nsym; base += 256) {
-        const int64_t m = base + threadIdx.x;
-        if (m < p.nsym) sidx[threadIdx.x] = tx_symbol_index(p, m);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const int cnt = (int)(p.nsym - base < 256 ? p.nsym - base : 256);
-            for (int j = 0; j < cnt; ++j) {
-                st = scan_step_any(k, st, sidx[j], p.s0 + (uint64_t)(base + j) * (uint64_t)p.sps + 1u);
-                sst[j] = st;
-            }
-        }
-        __syncthreads();
-        if (m < p.nsym) p.scan[m] = sst[threadIdx.x];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) p.hist_new[0] = st;
-}
 
 // A bank of channels of one scanned kind (modem_tx_process_batch): one lane of wave 0 per channel
 // (kScanCpw channels per workgroup) runs that channel's recurrence with scan_step — the same operations in
@@ -332,14 +304,17 @@ __global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
 // waves, not the recurrences, bounded a 64-channel workgroup (a bank of 64 DMPSK channels 352 ->
 // 1090 Msymbols/s, MFSK 351 -> 682, BFSK 400 -> 490; 8 per workgroup measured the same as 16).
 // ps: the channels' parameter blocks in device memory.
+// A single channel (tx_scan) runs the same body with one channel per workgroup: lane 0 of wave 0
+// runs the recurrence while wave 1 streams (the earlier single form, every lane decoding 256
+// indices, then lane 0 stepping, then every lane storing, serially: 6-9 Msymbols/s).
+// scan_bank: channels ps[0 .. nc) (nc <= CPW) in this workgroup.
 constexpr int kScanCpw = 16;
-template <int KIND>
-__global__ __launch_bounds__(256) void tx_scan_batch(const TxParams* __restrict__ ps, int nch) {
+template <int KIND, int CPW>
+__device__ __forceinline__ void scan_bank(const TxParams* __restrict__ ps, int nc) {
     constexpr int B = 64, S = B + 1;           // symbols per block; LDS row stride (conflict-free columns)
-    __shared__ uint32_t sidx[2][kScanCpw * S];
-    __shared__ float2 sst[2][kScanCpw * S];
-    const int c0 = (int)blockIdx.x * kScanCpw;
-    const int nc = nch - c0 < kScanCpw ? nch - c0 : kScanCpw;
+    __shared__ uint32_t sidx[2][CPW * S];
+    __shared__ float2 sst[2][CPW * S];
+    const int c0 = 0;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     int64_t nmax = 0;
     for (int c = 0; c < nc; ++c) nmax = ps[c0 + c].nsym > nmax ? ps[c0 + c].nsym : nmax;
@@ -402,6 +377,18 @@ __global__ __launch_bounds__(256) void tx_scan_batch(const TxParams* __restrict_
     }
     if (wave > 0 && nblk > 0) store_block(nblk - 1);
     if (wave == 0 && lane < nc) ps[c0 + lane].hist_new[0] = st;
+}
+template <int KIND>
+__global__ __launch_bounds__(256) void tx_scan_batch(const TxParams* __restrict__ ps, int nch) {
+    const int c0 = (int)blockIdx.x * kScanCpw;
+    scan_bank<KIND, kScanCpw>(ps + c0, nch - c0 < kScanCpw ? nch - c0 : kScanCpw);
+}
+template <int KIND>
+__global__ __launch_bounds__(256) void tx_scan(const TxParams p) {
+    __shared__ TxParams sp;                    // the parameter block where the body's loads reach it
+    if (threadIdx.x == 0) sp = p;
+    __syncthreads();
+    scan_bank<KIND, 1>(&sp, 1);
 }
 
 hipError_t launch_tx_scan_batch(const TxParams* dps, int nch, int kind, hipStream_t s) {
@@ -474,7 +461,12 @@ __global__ __launch_bounds__(256) void tx_phasor(const TxParams p) {
 hipError_t launch_tx_phasor(const TxParams& p, int dtype, int out_mode, hipStream_t s, bool scanned) {
     const int64_t nsamp = p.nsym * p.sps;
     if (p.scan != nullptr && !scanned) {
-        hipLaunchKernelGGL(tx_scan, dim3(1), dim3(256), 0, s, p);
+        switch (p.ph_kind) {
+        case PH_DMPSK: hipLaunchKernelGGL(tx_scan<PH_DMPSK>, dim3(1), dim3(256), 0, s, p); break;
+        case PH_MFSK: hipLaunchKernelGGL(tx_scan<PH_MFSK>, dim3(1), dim3(256), 0, s, p); break;
+        case PH_BFSK: hipLaunchKernelGGL(tx_scan<PH_BFSK>, dim3(1), dim3(256), 0, s, p); break;
+        default: return hipErrorInvalidValue;
+        }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
